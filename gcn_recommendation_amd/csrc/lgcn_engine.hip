@@ -1,0 +1,714 @@
+// lgcn_engine.hip — MI355X (gfx950, CDNA4) kernels + C ABI for LightGCN propagation.
+//
+// Replaces, for a HIP device, the reference hot path (models/lightgcn.py:37-59 and
+// models/lightgcn_fusion.py:132-142): E_{k+1} = Â·E_k for K layers (torch.sparse.mm, lightgcn.py:45),
+// the layer mean (lightgcn.py:54), and the autograd backward of both. Declarations and the
+// numerics contract: include/lgcn.h. Design and byte model: DESIGN.md.
+//
+// Kernel shape (HBM-bound sparse gather-reduce, no MFMA):
+//  * a row of Â is owned by a group of G lanes (G = d/4 rounded to a power of two, <= 64), each
+//    lane holding NV float4 columns of the output row: a gathered 256-B row of X at d=64 is ONE
+//    coalesced 16-lane dwordx4 access; a wave64 works on 64/G rows at once.
+//  * each group walks its row's 8-byte {col,val} edge records in stored order, issues U gathers
+//    before consuming any (memory-level parallelism), then folds them with v_fma_f32 in order —
+//    the same sequential fmaf chain ATen's CPU addmm_sparse_dense loop runs, so results are bitwise
+//    identical to the reference CPU path for every row the chain covers.
+//  * rows longer than hub_threshold are cut into chunks (host plan) that run in the SAME launch
+//    (blocks [0, hub_blocks)), writing partial sums; k_hub_combine finishes them in fixed order.
+//  * the epilogue is fused: store, the K+1-layer mean (reads E0..E_{K-1} rows, sums in order,
+//    divides), or the backward's Horner add. E0 is read as three segments (no torch.cat copy).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <stdint.h>
+#include <string.h>
+
+#include "lgcn.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------------------------
+// small vector helpers: V = float4 (vector path) or float (scalar path)
+// ---------------------------------------------------------------------------------------------
+template <typename V> struct VT;
+template <> struct VT<float4> {
+    static constexpr int W = 4;
+    __device__ static float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+    __device__ static float4 load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+    __device__ static void store(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+    __device__ static float4 fma(float a, float4 x, float4 y) {
+        return make_float4(__builtin_fmaf(a, x.x, y.x), __builtin_fmaf(a, x.y, y.y),
+                           __builtin_fmaf(a, x.z, y.z), __builtin_fmaf(a, x.w, y.w));
+    }
+    __device__ static float4 add(float4 a, float4 b) {
+        return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    __device__ static float4 div(float4 a, float b) {
+        return make_float4(a.x / b, a.y / b, a.z / b, a.w / b);
+    }
+};
+template <> struct VT<float> {
+    static constexpr int W = 1;
+    __device__ static float zero() { return 0.f; }
+    __device__ static float load(const float* p) { return *p; }
+    __device__ static void store(float* p, float v) { *p = v; }
+    __device__ static float fma(float a, float x, float y) { return __builtin_fmaf(a, x, y); }
+    __device__ static float add(float a, float b) { return a + b; }
+    __device__ static float div(float a, float b) { return a / b; }
+};
+
+__device__ __forceinline__ const float* seg_row(const lgcn_rows_t& s, int32_t r) {
+    if (r < s.end0) return s.p0 + (int64_t)r * s.ld;
+    if (r < s.end1) return s.p1 + (int64_t)(r - s.end0) * s.ld;
+    return s.p2 + (int64_t)(r - s.end1) * s.ld;
+}
+
+__device__ __forceinline__ int2 load_edge(const lgcn_edge_t* e) {
+    return *reinterpret_cast<const int2*>(e);
+}
+
+// Sequential fmaf chain over edge records [beg, end) — the ATen CPU order (one row's nonzeros in
+// stored order, y = fma(val, x, y) starting from +0). U gathers are in flight before the folds.
+template <typename V, int G, int NV, int U>
+__device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges, int32_t beg,
+                                           int32_t end, const lgcn_rows_t& x, int lane, int dW,
+                                           V (&acc)[NV]) {
+    using T = VT<V>;
+    for (int32_t j = beg; j < end; j += U) {
+        const int n = min(U, end - j);
+        int2 e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) e[u] = (u < n) ? load_edge(edges + j + u) : make_int2(0, 0);
+        V xv[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float* rp = seg_row(x, e[u].x);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int c = lane + q * G;
+                xv[u][q] = (u < n && c < dW) ? T::load(rp + c * T::W) : T::zero();
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u < n) {
+                const float v = __int_as_float(e[u].y);
+#pragma unroll
+                for (int q = 0; q < NV; ++q) acc[q] = T::fma(v, xv[u][q], acc[q]);
+            }
+        }
+    }
+}
+
+// Fused epilogue for one output row (lanes of the row's group).
+template <typename V, int G, int NV, int MODE>
+__device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_t row, int lane,
+                                               int dW, V (&acc)[NV], float* __restrict__ y,
+                                               int64_t ldy) {
+    using T = VT<V>;
+    float* yr = y + (int64_t)row * ldy;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        const int c = lane + q * G;
+        if (c >= dW) continue;
+        V out = acc[q];
+        if constexpr (MODE == LGCN_EPI_MEAN) {
+            // ((E0 + E1) + ... + E_{K-1}) + E_K, then / (K+1): torch.mean(torch.stack(.), 0)
+            V s = T::load(seg_row(ep.prev0, row) + c * T::W);
+            for (int i = 0; i + 1 < ep.n_prev; ++i)
+                s = T::add(s, T::load(ep.prev_dense[i] + (int64_t)row * ep.ld_prev + c * T::W));
+            s = T::add(s, out);
+            out = T::div(s, ep.div);
+        } else if constexpr (MODE == LGCN_EPI_ADD) {
+            out = T::add(T::load(ep.addend + (int64_t)row * ep.ld_add + c * T::W), out);
+        }
+        T::store(yr + c * T::W, out);
+    }
+}
+
+template <typename V, int G, int NV, int MODE>
+__global__ __launch_bounds__(kBlock) void k_layer(
+    const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
+    int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
+    int32_t hub_blocks, float* __restrict__ partials, lgcn_rows_t x, float* __restrict__ y,
+    int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep) {
+    using T = VT<V>;
+    constexpr int RPB = kBlock / G;
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = threadIdx.x / G;
+    V acc[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) acc[q] = T::zero();
+
+    if ((int32_t)blockIdx.x < hub_blocks) {  // hub chunks first: the longest work starts earliest
+        const int32_t it = blockIdx.x * RPB + grp;
+        if (it >= n_items) return;
+        const lgcn_hub_item_t w = items[it];
+        accumulate<V, G, NV, U>(edges, w.beg, w.end, x, lane, dW, acc);
+        float* pr = partials + (int64_t)w.slot * d;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int c = lane + q * G;
+            if (c < dW) T::store(pr + c * T::W, acc[q]);
+        }
+        return;
+    }
+    const int32_t row = (int32_t)(blockIdx.x - hub_blocks) * RPB + grp;
+    if (row >= n_rows) return;
+    const int32_t beg = rowptr[row];
+    const int32_t end = rowptr[row + 1];
+    if (end - beg > hub_thr) return;  // owned by the hub chunks + k_hub_combine
+    accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
+    epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
+}
+
+// One block per hub row: group g sums slots g, g+NG, ... in order; groups are then added in
+// group order. Deterministic (fixed order), not the CPU's single chain.
+template <typename V, int G, int NV, int MODE>
+__global__ __launch_bounds__(kBlock) void k_hub_combine(const lgcn_hub_row_t* __restrict__ rows,
+                                                        const float* __restrict__ partials,
+                                                        float* __restrict__ y, int64_t ldy,
+                                                        int32_t d, int32_t dW, lgcn_epilogue_t ep) {
+    using T = VT<V>;
+    constexpr int NG = kBlock / G;
+    __shared__ V red[NG][G * NV];
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = threadIdx.x / G;
+    const lgcn_hub_row_t hr = rows[blockIdx.x];
+    V acc[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) acc[q] = T::zero();
+    for (int s = grp; s < hr.n_slots; s += NG) {
+        const float* pr = partials + (int64_t)(hr.first_slot + s) * d;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int c = lane + q * G;
+            if (c < dW) acc[q] = T::add(acc[q], T::load(pr + c * T::W));
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[grp][lane + q * G] = acc[q];
+    __syncthreads();
+    if (grp != 0) return;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        V t = red[0][lane + q * G];
+        for (int g = 1; g < NG; ++g) t = T::add(t, red[g][lane + q * G]);
+        acc[q] = t;
+    }
+    epilogue_store<V, G, NV, MODE>(ep, hr.row, lane, dW, acc, y, ldy);
+}
+
+template <typename V, int G, int NV>
+__global__ __launch_bounds__(kBlock) void k_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t dW,
+                                                       float div, float* __restrict__ y,
+                                                       int64_t ldy) {
+    using T = VT<V>;
+    constexpr int RPB = kBlock / G;
+    const int lane = threadIdx.x & (G - 1);
+    const int32_t row = blockIdx.x * RPB + threadIdx.x / G;
+    if (row >= n_rows) return;
+    const float* xr = seg_row(x, row);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        const int c = lane + q * G;
+        if (c < dW) T::store(y + (int64_t)row * ldy + c * T::W, T::div(T::load(xr + c * T::W), div));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// COO -> CSR preparation kernels
+// ---------------------------------------------------------------------------------------------
+__global__ void k_coo_inspect(const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
+                              int64_t nnz, int32_t n_rows, int32_t n_cols, int32_t* flags) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    const int64_t r = rows[j], c = cols[j];
+    int f = 0;
+    if (r < 0 || r >= n_rows || c < 0 || c >= n_cols) f |= LGCN_COO_OUT_OF_RANGE;
+    if (j > 0) {
+        const int64_t rp = rows[j - 1];
+        if (r < rp) f |= LGCN_COO_ROWS_UNSORTED;
+        else if (r == rp && c <= cols[j - 1]) f |= LGCN_COO_COLS_UNSORTED;
+    }
+    if (f) atomicOr(flags, f);
+}
+
+__global__ void k_csr_edges(const int64_t* __restrict__ other, const float* __restrict__ vals,
+                            int64_t nnz, const int32_t* __restrict__ perm,
+                            lgcn_edge_t* __restrict__ edges) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    const int64_t src = perm ? perm[j] : j;
+    const uint32_t c = (uint32_t)other[src];
+    const uint32_t v = __float_as_uint(vals[src]);
+    edges[j] = (lgcn_edge_t)(((uint64_t)v << 32) | c);
+}
+
+// rowptr[r] = first j with key(j) >= r (binary search; keys sorted): no atomics, deterministic.
+__global__ void k_csr_rowptr(const int64_t* __restrict__ keys64, const int32_t* __restrict__ keys32,
+                             int64_t nnz, int32_t n_rows, int32_t* __restrict__ rowptr) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > n_rows) return;
+    int64_t lo = 0, hi = nnz;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int64_t k = keys32 ? (int64_t)keys32[mid] : keys64[mid];
+        if (k < r) lo = mid + 1; else hi = mid;
+    }
+    rowptr[r] = (int32_t)lo;
+}
+
+__global__ void k_keys_iota(const int64_t* __restrict__ keys, int64_t nnz, int32_t* __restrict__ k32,
+                            int32_t* __restrict__ perm) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    k32[j] = (int32_t)keys[j];
+    perm[j] = (int32_t)j;
+}
+
+__global__ void k_csr_symmetric(const int32_t* __restrict__ rowptr,
+                                const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
+                                int64_t nnz, int32_t* asym) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    // row of edge j: last r with rowptr[r] <= j
+    int32_t lo = 0, hi = n_rows - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        if (rowptr[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    const int32_t r = lo;
+    const int2 e = load_edge(edges + j);
+    const int32_t c = e.x;
+    int32_t a = rowptr[c], b = rowptr[c + 1];
+    while (a < b) {
+        const int32_t mid = (a + b) >> 1;
+        if (load_edge(edges + mid).x < r) a = mid + 1; else b = mid;
+    }
+    if (a >= rowptr[c + 1] || load_edge(edges + a).x != r || load_edge(edges + a).y != e.y)
+        atomicOr(asym, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------------------------
+inline int herr(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+inline int last_err() { return herr(hipGetLastError()); }
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Launch geometry from d: (vector?) G lanes per row, NV elements-of-V per lane.
+struct Geo {
+    bool vec;
+    int G;
+    int NV;
+    int dW;
+};
+
+inline int next_pow2(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+inline Geo pick_geo(int d, bool vec_ok) {
+    Geo g;
+    g.vec = vec_ok && (d % 4 == 0);
+    g.dW = g.vec ? d / 4 : d;
+    g.G = next_pow2(g.dW);
+    if (g.G < 4) g.G = 4;
+    if (g.G > 64) g.G = 64;
+    int nv = (g.dW + g.G - 1) / g.G;
+    g.NV = next_pow2(nv);
+    return g;
+}
+
+bool rows_aligned(const lgcn_rows_t& r) {
+    return al16(r.p0) && al16(r.p1) && al16(r.p2) && (r.ld % 4 == 0);
+}
+
+bool epi_aligned(const lgcn_epilogue_t& ep) {
+    if (ep.mode == LGCN_EPI_MEAN) {
+        if (!rows_aligned(ep.prev0) || ep.ld_prev % 4) return false;
+        for (int i = 0; i + 1 < ep.n_prev; ++i)
+            if (!al16(ep.prev_dense[i])) return false;
+    }
+    if (ep.mode == LGCN_EPI_ADD && (!al16(ep.addend) || ep.ld_add % 4)) return false;
+    return true;
+}
+
+template <typename V, int G, int NV>
+int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+                   const lgcn_hub_item_t* items, int32_t n_items, float* partials,
+                   const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
+                   const lgcn_epilogue_t& ep, hipStream_t s) {
+    constexpr int RPB = kBlock / G;
+    const int32_t hub_blocks = (n_items + RPB - 1) / RPB;
+    const int64_t row_blocks = ((int64_t)n_rows + RPB - 1) / RPB;
+    const int64_t grid = hub_blocks + row_blocks;
+    if (grid == 0) return 0;
+    if (grid > 0x7fffffffLL) return LGCN_EINVAL;
+    switch (ep.mode) {
+        case LGCN_EPI_STORE:
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_STORE>), dim3((uint32_t)grid), dim3(kBlock),
+                               0, s, rowptr, edges, n_rows, thr, items, n_items, hub_blocks,
+                               partials, x, y, ldy, d, dW, ep);
+            break;
+        case LGCN_EPI_MEAN:
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN>), dim3((uint32_t)grid), dim3(kBlock),
+                               0, s, rowptr, edges, n_rows, thr, items, n_items, hub_blocks,
+                               partials, x, y, ldy, d, dW, ep);
+            break;
+        case LGCN_EPI_ADD:
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD>), dim3((uint32_t)grid), dim3(kBlock),
+                               0, s, rowptr, edges, n_rows, thr, items, n_items, hub_blocks,
+                               partials, x, y, ldy, d, dW, ep);
+            break;
+        default:
+            return LGCN_EINVAL;
+    }
+    return last_err();
+}
+
+template <typename V, int G, int NV>
+int launch_combine_t(const lgcn_hub_row_t* rows, int32_t n, const float* partials, float* y,
+                     int64_t ldy, int32_t d, int32_t dW, const lgcn_epilogue_t& ep, hipStream_t s) {
+    if (n <= 0) return 0;
+    switch (ep.mode) {
+        case LGCN_EPI_STORE:
+            hipLaunchKernelGGL((k_hub_combine<V, G, NV, LGCN_EPI_STORE>), dim3(n), dim3(kBlock), 0, s,
+                               rows, partials, y, ldy, d, dW, ep);
+            break;
+        case LGCN_EPI_MEAN:
+            hipLaunchKernelGGL((k_hub_combine<V, G, NV, LGCN_EPI_MEAN>), dim3(n), dim3(kBlock), 0, s,
+                               rows, partials, y, ldy, d, dW, ep);
+            break;
+        case LGCN_EPI_ADD:
+            hipLaunchKernelGGL((k_hub_combine<V, G, NV, LGCN_EPI_ADD>), dim3(n), dim3(kBlock), 0, s,
+                               rows, partials, y, ldy, d, dW, ep);
+            break;
+        default:
+            return LGCN_EINVAL;
+    }
+    return last_err();
+}
+
+template <typename V, int G, int NV>
+int launch_scale_t(const lgcn_rows_t& x, int32_t n_rows, int32_t dW, float div, float* y,
+                   int64_t ldy, hipStream_t s) {
+    constexpr int RPB = kBlock / G;
+    const int64_t grid = ((int64_t)n_rows + RPB - 1) / RPB;
+    if (grid == 0) return 0;
+    hipLaunchKernelGGL((k_scale_rows<V, G, NV>), dim3((uint32_t)grid), dim3(kBlock), 0, s, x, n_rows,
+                       dW, div, y, ldy);
+    return last_err();
+}
+
+// Geometry dispatch: F is a generic lambda taking (V tag, G, NV) as template parameters via
+// a functor with a templated call operator.
+template <typename F>
+int dispatch_geo(const Geo& g, const F& f) {
+#define LGCN_CASE(VT_, G_, NV_) \
+    if (g.G == G_ && g.NV == NV_) return f.template operator()<VT_, G_, NV_>();
+    if (g.vec) {
+        LGCN_CASE(float4, 4, 1)
+        LGCN_CASE(float4, 8, 1)
+        LGCN_CASE(float4, 16, 1)
+        LGCN_CASE(float4, 32, 1)
+        LGCN_CASE(float4, 64, 1)
+        LGCN_CASE(float4, 64, 2)
+        LGCN_CASE(float4, 64, 4)
+        LGCN_CASE(float4, 64, 8)
+    } else {
+        LGCN_CASE(float, 4, 1)
+        LGCN_CASE(float, 8, 1)
+        LGCN_CASE(float, 16, 1)
+        LGCN_CASE(float, 32, 1)
+        LGCN_CASE(float, 64, 1)
+        LGCN_CASE(float, 64, 2)
+        LGCN_CASE(float, 64, 4)
+        LGCN_CASE(float, 64, 8)
+        LGCN_CASE(float, 64, 16)
+        LGCN_CASE(float, 64, 32)
+    }
+#undef LGCN_CASE
+    return LGCN_EINVAL;
+}
+
+int check_epi(const lgcn_epilogue_t* ep) {
+    if (!ep) return LGCN_EINVAL;
+    if (ep->mode < LGCN_EPI_STORE || ep->mode > LGCN_EPI_ADD) return LGCN_EINVAL;
+    if (ep->mode == LGCN_EPI_MEAN) {
+        if (ep->n_prev < 1) return LGCN_EINVAL;
+        if (ep->n_prev - 1 > LGCN_MAX_LAYERS) return LGCN_ETOOMANY;
+        if (!(ep->div > 0.f)) return LGCN_EINVAL;
+    }
+    if (ep->mode == LGCN_EPI_ADD && !ep->addend) return LGCN_EINVAL;
+    return 0;
+}
+
+struct LayerF {
+    const int32_t* rowptr; const lgcn_edge_t* edges; int32_t n_rows, thr;
+    const lgcn_hub_item_t* items; int32_t n_items; float* partials; const lgcn_rows_t* x;
+    float* y; int64_t ldy; int32_t d, dW; const lgcn_epilogue_t* ep; hipStream_t s;
+    template <typename V, int G, int NV> int operator()() const {
+        return launch_layer_t<V, G, NV>(rowptr, edges, n_rows, thr, items, n_items, partials, *x,
+                                        y, ldy, d, dW, *ep, s);
+    }
+};
+
+struct CombineF {
+    const lgcn_hub_row_t* rows; int32_t n; const float* partials; float* y; int64_t ldy;
+    int32_t d, dW; const lgcn_epilogue_t* ep; hipStream_t s;
+    template <typename V, int G, int NV> int operator()() const {
+        return launch_combine_t<V, G, NV>(rows, n, partials, y, ldy, d, dW, *ep, s);
+    }
+};
+
+struct ScaleF {
+    const lgcn_rows_t* x; int32_t n; int32_t dW; float div; float* y; int64_t ldy; hipStream_t s;
+    template <typename V, int G, int NV> int operator()() const {
+        return launch_scale_t<V, G, NV>(*x, n, dW, div, y, ldy, s);
+    }
+};
+
+int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+               const lgcn_hub_item_t* items, int32_t n_items, float* partials, lgcn_rows_t x,
+               float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+    const bool vec_ok = rows_aligned(x) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep) &&
+                        (n_items == 0 || al16(partials));
+    const Geo g = pick_geo(d, vec_ok);
+    LayerF f{rowptr, edges, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW, &ep, s};
+    return dispatch_geo(g, f);
+}
+
+int hub_combine(const lgcn_hub_row_t* rows, int32_t n, const float* partials, float* y,
+                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+    if (n <= 0) return 0;
+    const bool vec_ok = al16(partials) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep);
+    const Geo g = pick_geo(d, vec_ok);
+    CombineF f{rows, n, partials, y, ldy, d, g.dW, &ep, s};
+    return dispatch_geo(g, f);
+}
+
+int scale_rows(const lgcn_rows_t& x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
+               hipStream_t s) {
+    const bool vec_ok = rows_aligned(x) && al16(y) && (ldy % 4 == 0);
+    const Geo g = pick_geo(d, vec_ok);
+    ScaleF f{&x, n_rows, g.dW, div, y, ldy, s};
+    return dispatch_geo(g, f);
+}
+
+lgcn_rows_t dense_rows(const float* p, int32_t n, int64_t ld) {
+    lgcn_rows_t r;
+    r.p0 = r.p1 = r.p2 = p;
+    r.end0 = r.end1 = n;
+    r.ld = ld;
+    return r;
+}
+
+int valid_geom(int32_t n_rows, int32_t d) {
+    if (n_rows < 0 || d < 1 || d > 2048) return LGCN_EINVAL;
+    return 0;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+int lgcn_abi_version(void) { return LGCN_ABI_VERSION; }
+
+const char* lgcn_error_string(int code) {
+    switch (code) {
+        case 0: return "success";
+        case LGCN_EINVAL: return "lgcn: invalid argument";
+        case LGCN_EALIGN: return "lgcn: misaligned operand";
+        case LGCN_ETOOMANY: return "lgcn: too many layers for the fused mean epilogue";
+        default: break;
+    }
+    if (code > 0) return hipGetErrorString((hipError_t)code);
+    return "lgcn: unknown error";
+}
+
+int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host) {
+    hipDeviceProp_t p;
+    const hipError_t e = hipGetDeviceProperties(&p, device);
+    if (e != hipSuccess) return (int)e;
+    if (n_cu_host) *n_cu_host = p.multiProcessorCount;
+    if (arch_major_host) *arch_major_host = p.major;
+    return 0;
+}
+
+int lgcn_coo_inspect(const int64_t* rows, const int64_t* cols, int64_t nnz, int32_t n_rows,
+                     int32_t n_cols, int32_t* flags, void* stream) {
+    if (nnz < 0 || !flags) return LGCN_EINVAL;
+    if (nnz == 0) return 0;
+    if (!rows || !cols) return LGCN_EINVAL;
+    const int64_t grid = (nnz + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_coo_inspect, dim3((uint32_t)grid), dim3(kBlock), 0, S(stream), rows, cols,
+                       nnz, n_rows, n_cols, flags);
+    return last_err();
+}
+
+int lgcn_coo_to_csr(const int64_t* rows, const int64_t* cols, const float* vals, int64_t nnz,
+                    int32_t n_rows, const int32_t* perm, const int32_t* keys_sorted,
+                    int32_t* rowptr, lgcn_edge_t* edges, void* stream) {
+    if (nnz < 0 || nnz > 0x7fffffffLL || n_rows < 0 || !rowptr) return LGCN_EINVAL;
+    if (nnz > 0 && (!cols || !vals || !edges || (!rows && !keys_sorted))) return LGCN_EINVAL;
+    if ((perm == nullptr) != (keys_sorted == nullptr)) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (nnz > 0) {
+        hipLaunchKernelGGL(k_csr_edges, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, cols, vals, nnz, perm, edges);
+        if (int e = last_err()) return e;
+    }
+    const int64_t nr = (int64_t)n_rows + 1;
+    hipLaunchKernelGGL(k_csr_rowptr, dim3((uint32_t)((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, keys_sorted ? nullptr : rows, keys_sorted, nnz, n_rows, rowptr);
+    return last_err();
+}
+
+int lgcn_coo_sort_perm(const int64_t* keys, int64_t nnz, int32_t n_keys, int32_t* keys_tmp,
+                       int32_t* keys_sorted, int32_t* perm_tmp, int32_t* perm, void* temp,
+                       size_t* temp_bytes_host, void* stream) {
+    if (nnz < 0 || nnz > 0x7fffffffLL || !temp_bytes_host || n_keys < 0) return LGCN_EINVAL;
+    int end_bit = 1;
+    while (end_bit < 31 && (1LL << end_bit) < (int64_t)n_keys) ++end_bit;
+    hipStream_t s = S(stream);
+    if (temp == nullptr) {
+        size_t bytes = 0;
+        const hipError_t e = hipcub::DeviceRadixSort::SortPairs(
+            nullptr, bytes, keys_tmp, keys_sorted, perm_tmp, perm, (int)nnz, 0, end_bit, s);
+        *temp_bytes_host = bytes;
+        return herr(e);
+    }
+    if (nnz == 0) return 0;
+    if (!keys || !keys_tmp || !keys_sorted || !perm_tmp || !perm) return LGCN_EINVAL;
+    hipLaunchKernelGGL(k_keys_iota, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, keys, nnz, keys_tmp, perm_tmp);
+    if (int e = last_err()) return e;
+    size_t bytes = *temp_bytes_host;
+    // LSD radix sort: stable, so equal keys keep their stored order (torch's summation order).
+    return herr(hipcub::DeviceRadixSort::SortPairs(temp, bytes, keys_tmp, keys_sorted, perm_tmp,
+                                                   perm, (int)nnz, 0, end_bit, s));
+}
+
+int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
+                             int64_t nnz, int32_t* asym, void* stream) {
+    if (!rowptr || !asym || n_rows < 0 || nnz < 0) return LGCN_EINVAL;
+    if (nnz == 0 || n_rows == 0) return 0;
+    hipLaunchKernelGGL(k_csr_symmetric, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, S(stream), rowptr, edges, n_rows, nnz, asym);
+    return last_err();
+}
+
+int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
+                    int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
+                    float* partials, lgcn_rows_t x, float* y, int64_t ldy, int32_t d,
+                    const lgcn_epilogue_t* epi_host, void* stream) {
+    if (int e = valid_geom(n_rows, d)) return e;
+    if (int e = check_epi(epi_host)) return e;
+    if (n_rows > 0 && (!rowptr || !y || ldy < d)) return LGCN_EINVAL;
+    if (n_hub_items < 0 || (n_hub_items > 0 && (!hub_items || !partials))) return LGCN_EINVAL;
+    return spmm_layer(rowptr, edges, n_rows, hub_threshold, hub_items, n_hub_items, partials, x, y,
+                      ldy, d, *epi_host, S(stream));
+}
+
+int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
+                     float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                     void* stream) {
+    if (d < 1 || d > 2048 || n_hub_rows < 0) return LGCN_EINVAL;
+    if (int e = check_epi(epi_host)) return e;
+    if (n_hub_rows > 0 && (!hub_rows || !partials || !y || ldy < d)) return LGCN_EINVAL;
+    return hub_combine(hub_rows, n_hub_rows, partials, y, ldy, d, *epi_host, S(stream));
+}
+
+int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
+                    void* stream) {
+    if (int e = valid_geom(n_rows, d)) return e;
+    if (n_rows > 0 && (!y || ldy < d)) return LGCN_EINVAL;
+    return scale_rows(x, n_rows, d, div, y, ldy, S(stream));
+}
+
+int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+                           int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
+                           int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
+                           int32_t n_hub_rows, float* partials, lgcn_rows_t emb, int32_t d,
+                           int32_t K, float* const* layer_bufs_host, float* out,
+                           void* const* ev_host, void* stream) {
+    if (int e = valid_geom(n, d)) return e;
+    if (K < 0 || K - 1 > LGCN_MAX_LAYERS || !out) return K < 0 || !out ? LGCN_EINVAL : LGCN_ETOOMANY;
+    if (K > 1 && !layer_bufs_host) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (K == 0) return scale_rows(emb, n, d, 1.0f, out, d, s);
+    for (int k = 1; k <= K; ++k) {
+        const lgcn_rows_t x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
+        lgcn_epilogue_t ep;
+        memset(&ep, 0, sizeof(ep));
+        float* y;
+        if (k < K) {
+            ep.mode = LGCN_EPI_STORE;
+            y = layer_bufs_host[k - 1];
+        } else {
+            ep.mode = LGCN_EPI_MEAN;
+            ep.n_prev = K;
+            ep.div = (float)(K + 1);
+            ep.prev0 = emb;
+            for (int i = 0; i + 1 < K; ++i) ep.prev_dense[i] = layer_bufs_host[i];
+            ep.ld_prev = d;
+            y = out;
+        }
+        if (ev_host) {
+            if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1)], s))) return e;
+        }
+        if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials, x,
+                               y, d, d, ep, s))
+            return e;
+        if (ev_host) {
+            if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1) + 1], s))) return e;
+        }
+        if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;
+    }
+    return 0;
+}
+
+int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
+                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
+                            int32_t n_hub_rows, float* partials, const float* grad_out,
+                            int32_t d, int32_t K, float* work_c, float* work_h, float* grad_e0,
+                            void* stream) {
+    if (int e = valid_geom(n, d)) return e;
+    if (K < 0 || !grad_out || !grad_e0) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    const lgcn_rows_t g = dense_rows(grad_out, n, d);
+    if (K == 0) return scale_rows(g, n, d, 1.0f, grad_e0, d, s);
+    if (!work_c || (K > 1 && !work_h)) return LGCN_EINVAL;
+    // MeanBackward: every stacked layer receives G / (K+1)
+    if (int e = scale_rows(g, n, d, (float)(K + 1), work_c, d, s)) return e;
+    const float* h = work_c;
+    for (int k = 1; k <= K; ++k) {
+        float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
+        lgcn_epilogue_t ep;
+        memset(&ep, 0, sizeof(ep));
+        ep.mode = LGCN_EPI_ADD;
+        ep.addend = work_c;
+        ep.ld_add = d;
+        if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials,
+                               dense_rows(h, n, d), y, d, d, ep, s))
+            return e;
+        if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;
+        h = y;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,419 @@
+"""Host side of the MI355X LightGCN propagation engine: ctypes binding of liblgcn_engine.so
+(include/lgcn.h), the cached COO->CSR graph plan, and the autograd Function that replaces
+
+    ego = torch.cat([user, item, brand]); for k < K: ego = torch.sparse.mm(adj, ego)
+    final = torch.mean(torch.stack(all_layers), 0)           (models/lightgcn.py:37-54)
+
+on a HIP device. There is no fallback: if the extension is missing or a launch fails, the call
+raises. The library is loaded after `import torch`, so its libamdhip64.so.7 dependency binds to
+the HIP runtime torch already loaded.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+import torch
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "liblgcn_engine.so")
+
+# ---- ABI mirrors (include/lgcn.h) -------------------------------------------------------------
+LGCN_EPI_STORE, LGCN_EPI_MEAN, LGCN_EPI_ADD = 0, 1, 2
+LGCN_MAX_LAYERS = 16
+COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
+INT32_MAX = 2 ** 31 - 1
+
+# Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
+# longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
+DEFAULT_HUB_THRESHOLD = 512
+DEFAULT_HUB_CHUNK = 256
+
+
+class RowsT(ctypes.Structure):
+    _fields_ = [("p0", ctypes.c_void_p), ("p1", ctypes.c_void_p), ("p2", ctypes.c_void_p),
+                ("end0", ctypes.c_int32), ("end1", ctypes.c_int32), ("ld", ctypes.c_int64)]
+
+
+class EpilogueT(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("n_prev", ctypes.c_int32), ("div", ctypes.c_float),
+                ("pad", ctypes.c_int32), ("prev0", RowsT),
+                ("prev_dense", ctypes.c_void_p * LGCN_MAX_LAYERS), ("ld_prev", ctypes.c_int64),
+                ("addend", ctypes.c_void_p), ("ld_add", ctypes.c_int64)]
+
+
+class LgcnError(RuntimeError):
+    pass
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+# (name, restype, argtypes) — every symbol include/lgcn.h declares
+_P, _I32, _I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+ABI = [
+    ("lgcn_abi_version", ctypes.c_int, []),
+    ("lgcn_error_string", ctypes.c_char_p, [ctypes.c_int]),
+    ("lgcn_device_info", ctypes.c_int, [ctypes.c_int, _P, _P]),
+    ("lgcn_coo_inspect", ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
+    ("lgcn_coo_to_csr", ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P]),
+    ("lgcn_coo_sort_perm", ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P,
+                                          ctypes.POINTER(ctypes.c_size_t), _P]),
+    ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
+    ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, RowsT, _P, _I64, _I32,
+                                       ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _P, _P, _I64, _I32,
+                                        ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
+    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, RowsT,
+                                              _I32, _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, _P,
+                                               _I32, _I32, _P, _P, _P, _P]),
+]
+
+
+def load_library(path=None):
+    """Load liblgcn_engine.so (built by __graft_entry__.build()). Raises if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise LgcnError(f"liblgcn_engine.so not found at {p}: run `python -c \"import "
+                            f"__graft_entry__ as g; g.build()\"` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(p)
+        for name, res, args in ABI:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.lgcn_abi_version() != 1:
+            raise LgcnError("liblgcn_engine.so ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = _lib.lgcn_error_string(rc).decode() if _lib is not None else str(rc)
+        raise LgcnError(f"{what} failed: {msg} (code {rc})")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def rows_desc(segments, ld):
+    """lgcn_rows_t over 1..3 row segments (each [rows x d] with leading dim ld)."""
+    if len(segments) == 1:
+        t = segments[0]
+        return RowsT(t.data_ptr(), t.data_ptr(), t.data_ptr(), t.shape[0], t.shape[0], ld)
+    ps, ends, acc = [], [], 0
+    for t in segments:
+        ps.append(t.data_ptr())
+        acc += t.shape[0]
+        ends.append(acc)
+    while len(ps) < 3:
+        ps.append(ps[-1])
+        ends.append(ends[-1])
+    return RowsT(ps[0], ps[1], ps[2], ends[0], ends[1], ld)
+
+
+def hub_threshold_from_env(default=DEFAULT_HUB_THRESHOLD):
+    v = os.environ.get("LGCN_HUB_THRESHOLD", "")
+    if v.lower() in ("exact", "inf", "none", "off"):
+        return INT32_MAX
+    return int(v) if v else default
+
+
+# ----------------------------------------------------------------------------------------------
+# graph plan: CSR + hub chunks, built once per adjacency tensor and cached on it
+# ----------------------------------------------------------------------------------------------
+class HubPlan:
+    def __init__(self, threshold, chunk, items, rows, n_slots):
+        self.threshold = threshold
+        self.chunk = chunk
+        self.items = items      # int32 [n_items, 4] device (lgcn_hub_item_t)
+        self.rows = rows        # int32 [n_rows, 4] device (lgcn_hub_row_t)
+        self.n_items = 0 if items is None else items.shape[0]
+        self.n_rows = 0 if rows is None else rows.shape[0]
+        self.n_slots = n_slots
+
+
+def plan_hubs(rowptr_host, threshold, chunk, device):
+    """Cut rows with degree > threshold into `chunk`-edge pieces (host planner, numpy)."""
+    deg = np.diff(rowptr_host.astype(np.int64))
+    hub = np.nonzero(deg > threshold)[0]
+    if threshold >= INT32_MAX or hub.size == 0:
+        return HubPlan(threshold, chunk, None, None, 0)
+    nch = (deg[hub] + chunk - 1) // chunk
+    first = np.concatenate([[0], np.cumsum(nch)[:-1]])
+    n_slots = int(nch.sum())
+    row_of = np.repeat(hub, nch)
+    k = np.arange(n_slots) - np.repeat(first, nch)
+    beg = rowptr_host[row_of].astype(np.int64) + k * chunk
+    end = np.minimum(beg + chunk, rowptr_host[row_of + 1])
+    # longest rows first so their combine inputs are ready early; items in slot order
+    items = np.stack([row_of, beg, end, np.arange(n_slots)], 1).astype(np.int32)
+    rows = np.stack([hub, first, nch, np.zeros_like(hub)], 1).astype(np.int32)
+    return HubPlan(threshold, chunk, torch.from_numpy(items).to(device),
+                   torch.from_numpy(rows).to(device), n_slots)
+
+
+class Graph:
+    """Device CSR of a square Â plus its backward operator (Âᵀ, == Â when bitwise symmetric)."""
+
+    def __init__(self, n_rows, n_cols, rowptr, edges, nnz, device):
+        self.n_rows, self.n_cols, self.nnz = n_rows, n_cols, nnz
+        self.rowptr, self.edges, self.device = rowptr, edges, device
+        self.transpose = None
+        self.symmetric = None
+        self._plans = {}
+        self._rowptr_host = None
+
+    def rowptr_host(self):
+        if self._rowptr_host is None:
+            self._rowptr_host = self.rowptr.cpu().numpy()
+        return self._rowptr_host
+
+    def hubs(self, threshold, chunk=DEFAULT_HUB_CHUNK):
+        key = (threshold, chunk)
+        if key not in self._plans:
+            self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device)
+        return self._plans[key]
+
+    def degrees(self):
+        return np.diff(self.rowptr_host().astype(np.int64))
+
+
+def _coo_to_csr(lib, key, other, vals, nnz, n_keys, device, stream, sort):
+    rowptr = torch.empty(n_keys + 1, dtype=torch.int32, device=device)
+    edges = torch.empty(max(nnz, 1), dtype=torch.int64, device=device)
+    perm = keys_sorted = None
+    if sort and nnz > 0:
+        keys_tmp = torch.empty(nnz, dtype=torch.int32, device=device)
+        keys_sorted = torch.empty(nnz, dtype=torch.int32, device=device)
+        perm_tmp = torch.empty(nnz, dtype=torch.int32, device=device)
+        perm = torch.empty(nnz, dtype=torch.int32, device=device)
+        nbytes = ctypes.c_size_t(0)
+        _check(lib.lgcn_coo_sort_perm(None, nnz, n_keys, _ptr(keys_tmp), _ptr(keys_sorted),
+                                      _ptr(perm_tmp), _ptr(perm), None, ctypes.byref(nbytes),
+                                      stream), "lgcn_coo_sort_perm(size)")
+        temp = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
+        _check(lib.lgcn_coo_sort_perm(_ptr(key), nnz, n_keys, _ptr(keys_tmp), _ptr(keys_sorted),
+                                      _ptr(perm_tmp), _ptr(perm), _ptr(temp), ctypes.byref(nbytes),
+                                      stream), "lgcn_coo_sort_perm")
+    _check(lib.lgcn_coo_to_csr(_ptr(key), _ptr(other), _ptr(vals), nnz, n_keys, _ptr(perm),
+                               _ptr(keys_sorted), _ptr(rowptr), _ptr(edges), stream),
+           "lgcn_coo_to_csr")
+    return rowptr, edges
+
+
+def graph_from_coo(adj):
+    """Convert the caller-owned sparse COO Â (main.py:334-336) into the engine's CSR, once.
+
+    The plan is cached on the tensor object and re-validated by storage pointers and version
+    counters, so the per-batch call `model(norm_adj_tensor)` (main.py:495) costs nothing extra.
+    """
+    if not adj.is_sparse or adj.layout != torch.sparse_coo:
+        raise LgcnError("adj_mat must be a torch.sparse_coo_tensor")
+    if adj.dim() != 2 or adj.shape[0] != adj.shape[1]:
+        raise LgcnError(f"adj_mat must be square 2-D, got {tuple(adj.shape)}")
+    if adj.dtype != torch.float32:
+        raise LgcnError(f"adj_mat must be float32, got {adj.dtype}")
+    idx = adj._indices()
+    vals = adj._values()
+    key = (idx.data_ptr(), vals.data_ptr(), idx._version, vals._version, adj._nnz(),
+           tuple(adj.shape), str(adj.device))
+    cached = getattr(adj, "_lgcn_graph", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    lib = load_library()
+    device = adj.device
+    n = int(adj.shape[0])
+    nnz = int(adj._nnz())
+    if n > INT32_MAX - 1 or nnz > INT32_MAX:
+        raise LgcnError("graph too large for int32 CSR")
+    with torch.cuda.device(device):
+        stream = _stream(device)
+        idx = idx.contiguous()
+        vals = vals.contiguous()
+        rows, cols = idx[0].contiguous(), idx[1].contiguous()
+        flags = torch.zeros(1, dtype=torch.int32, device=device)
+        _check(lib.lgcn_coo_inspect(_ptr(rows), _ptr(cols), nnz, n, n, _ptr(flags), stream),
+               "lgcn_coo_inspect")
+        f = int(flags.item())
+        if f & COO_OUT_OF_RANGE:
+            raise LgcnError("adj_mat has indices out of range")
+        rowptr, edges = _coo_to_csr(lib, rows, cols, vals, nnz, n, device, stream,
+                                    sort=bool(f & COO_ROWS_UNSORTED))
+        g = Graph(n, n, rowptr, edges, nnz, device)
+        symmetric = False
+        if not (f & (COO_ROWS_UNSORTED | COO_COLS_UNSORTED)):
+            asym = torch.zeros(1, dtype=torch.int32, device=device)
+            _check(lib.lgcn_csr_check_symmetric(_ptr(rowptr), _ptr(edges), n, nnz, _ptr(asym),
+                                                stream), "lgcn_csr_check_symmetric")
+            symmetric = int(asym.item()) == 0
+        g.symmetric = symmetric
+        if symmetric:
+            g.transpose = g
+        else:
+            # Âᵀ with each row's entries in Â's stored order (torch's sparse t() + addmm loop)
+            t_rowptr, t_edges = _coo_to_csr(lib, cols, rows, vals, nnz, n, device, stream,
+                                            sort=True)
+            g.transpose = Graph(n, n, t_rowptr, t_edges, nnz, device)
+            g.transpose.transpose = g
+    try:
+        adj._lgcn_graph = (key, g)
+    except (AttributeError, RuntimeError):
+        pass
+    return g
+
+
+# ----------------------------------------------------------------------------------------------
+# propagation
+# ----------------------------------------------------------------------------------------------
+def _epilogue(mode, prev0=None, prev_dense=(), ld_prev=0, div=1.0, addend=None, ld_add=0):
+    ep = EpilogueT()
+    ep.mode = mode
+    ep.div = div
+    if prev0 is not None:
+        ep.prev0 = prev0
+        ep.n_prev = 1 + len(prev_dense)
+        for i, t in enumerate(prev_dense):
+            ep.prev_dense[i] = t.data_ptr()
+        ep.ld_prev = ld_prev
+    if addend is not None:
+        ep.addend = addend.data_ptr()
+        ep.ld_add = ld_add
+    return ep
+
+
+def _check_emb(segments, d, device):
+    for t in segments:
+        if t.device != device:
+            raise LgcnError(f"embedding on {t.device}, adjacency on {device}")
+        if t.dtype != torch.float32:
+            raise LgcnError("embeddings must be float32")
+        if t.dim() != 2 or t.shape[1] != d or t.stride(1) != 1 or t.stride(0) != d:
+            raise LgcnError("embedding blocks must be contiguous [rows x d]")
+
+
+def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None):
+    """One layer Y = epilogue(Â·X) through lgcn_spmm_layer + lgcn_hub_combine."""
+    lib = load_library()
+    hp = hubs or graph.hubs(hub_threshold)
+    partials = None
+    if hp.n_items:
+        partials = torch.empty(hp.n_slots * d, dtype=torch.float32, device=graph.device)
+    stream = stream or _stream(graph.device)
+    x = rows_desc(x_segments, d)
+    _check(lib.lgcn_spmm_layer(_ptr(graph.rowptr), _ptr(graph.edges), graph.n_rows,
+                               min(hp.threshold, INT32_MAX), _ptr(hp.items), hp.n_items,
+                               _ptr(partials), x, _ptr(y), y.stride(0), d, ctypes.byref(epi),
+                               stream), "lgcn_spmm_layer")
+    if hp.n_rows:
+        _check(lib.lgcn_hub_combine(_ptr(hp.rows), hp.n_rows, _ptr(partials), _ptr(y), y.stride(0),
+                                    d, ctypes.byref(epi), stream), "lgcn_hub_combine")
+    return y
+
+
+def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
+                      return_layers=False):
+    """final = mean(E0, Â E0, ..., Â^K E0) with E0 = cat(segments) (never materialised).
+
+    layer_events: optional list of (start, end) torch.cuda.Event pairs recorded around each
+    layer's lgcn_spmm_layer launch on the current stream (bench.py's live kernel timing).
+    """
+    if hub_threshold is None:
+        hub_threshold = hub_threshold_from_env()
+    d = segments[0].shape[1]
+    n = sum(int(t.shape[0]) for t in segments)
+    if n != graph.n_rows:
+        raise LgcnError(f"embedding rows {n} != adjacency size {graph.n_rows}")
+    _check_emb(segments, d, graph.device)
+    if K > LGCN_MAX_LAYERS + 1 or K < 0:
+        raise LgcnError(f"n_layers={K} unsupported (0..{LGCN_MAX_LAYERS + 1})")
+    lib = load_library()
+    dev = graph.device
+    with torch.cuda.device(dev):
+        stream = _stream(dev)
+        e0 = rows_desc(segments, d)
+        out = torch.empty((n, d), dtype=torch.float32, device=dev)
+        if K == 0:
+            _check(lib.lgcn_scale_rows(e0, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
+            return (out, []) if return_layers else out
+        hp = graph.hubs(hub_threshold)
+        layers = [torch.empty((n, d), dtype=torch.float32, device=dev) for _ in range(K - 1)]
+        for k in range(1, K + 1):
+            xs = segments if k == 1 else [layers[k - 2]]
+            if k < K:
+                y, ep = layers[k - 1], _epilogue(LGCN_EPI_STORE)
+            else:
+                y = out
+                ep = _epilogue(LGCN_EPI_MEAN, prev0=e0, prev_dense=layers, ld_prev=d,
+                               div=float(K + 1))
+            if layer_events is not None:
+                layer_events[k - 1][0].record()
+            spmm_layer(graph, xs, y, d, ep, hub_threshold, hp, stream)
+            if layer_events is not None:
+                layer_events[k - 1][1].record()
+        return (out, layers) if return_layers else out
+
+
+def propagate_backward(graph, grad_out, K, hub_threshold=None):
+    """dE0 = Σ_k (Âᵀ)^k G/(K+1), Horner order h = G/(K+1) + Âᵀ h (autograd's accumulation)."""
+    if hub_threshold is None:
+        hub_threshold = hub_threshold_from_env()
+    gt = graph.transpose
+    n, d = grad_out.shape
+    g = grad_out.contiguous()
+    lib = load_library()
+    dev = graph.device
+    with torch.cuda.device(dev):
+        stream = _stream(dev)
+        out = torch.empty((n, d), dtype=torch.float32, device=dev)
+        if K == 0:
+            _check(lib.lgcn_scale_rows(rows_desc([g], d), n, d, 1.0, _ptr(out), d, stream),
+                   "lgcn_scale_rows")
+            return out
+        c = torch.empty((n, d), dtype=torch.float32, device=dev)
+        _check(lib.lgcn_scale_rows(rows_desc([g], d), n, d, float(K + 1), _ptr(c), d, stream),
+               "lgcn_scale_rows")
+        hp = gt.hubs(hub_threshold)
+        work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
+        h = c
+        ep = _epilogue(LGCN_EPI_ADD, addend=c, ld_add=d)
+        for k in range(1, K + 1):
+            y = out if (K - k) % 2 == 0 else work
+            spmm_layer(gt, [h], y, d, ep, hub_threshold, hp, stream)
+            h = y
+        return out
+
+
+class PropagateFunction(torch.autograd.Function):
+    """(user, item, brand) weights -> mean of K propagated layers; backward by the same kernel."""
+
+    @staticmethod
+    def forward(ctx, graph, K, hub_threshold, *segments):
+        ctx.graph, ctx.K, ctx.hub_threshold = graph, K, hub_threshold
+        ctx.sizes = [int(t.shape[0]) for t in segments]
+        segs = [t.detach() for t in segments]
+        return propagate_forward(graph, segs, K, hub_threshold)
+
+    @staticmethod
+    def backward(ctx, grad):
+        g = propagate_backward(ctx.graph, grad, ctx.K, ctx.hub_threshold)
+        return (None, None, None) + tuple(torch.split(g, ctx.sizes, 0))
+
+
+def propagate(adj, segments, K, hub_threshold=None):
+    """Autograd-aware engine entry used by models.LightGCN / LightGCN_Fusion on a HIP device."""
+    graph = graph_from_coo(adj)
+    if hub_threshold is None:
+        hub_threshold = hub_threshold_from_env()
+    return PropagateFunction.apply(graph, K, hub_threshold, *segments)

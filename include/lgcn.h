@@ -1,0 +1,183 @@
+/*
+ * lgcn.h — C ABI of the MI355X-native LightGCN propagation engine (liblgcn_engine.so, gfx950).
+ *
+ * The hot path this library replaces is the K-layer propagation of the reference model
+ *     ego = cat(user, item, brand)                         models/lightgcn.py:37-40
+ *     for k < K: ego = torch.sparse.mm(adj_mat, ego)       models/lightgcn.py:44-46
+ *     final = mean(stack([E0..EK]), 0)                     models/lightgcn.py:54
+ *     (and the identical loop, models/lightgcn_fusion.py:132-139)
+ * plus its autograd backward (torch SparseAddmmBackward0 + MeanBackward + CatBackward), and the
+ * one-time conversion of the caller-owned `torch.sparse_coo_tensor` Â (main.py:331-336) into the
+ * engine's CSR form. A ctypes binding of every entry point ships in
+ * gcn_recommendation_amd/engine.py; INTEGRATION.md shows how a maintainer binds it.
+ *
+ * Conventions
+ *  - Every pointer is a device pointer (hipMalloc / torch CUDA storage) unless named *_host.
+ *  - No entry point allocates, frees or synchronises. Work is enqueued on `stream`
+ *    (hipStream_t passed as void*; NULL = legacy default stream). Graph-capture safe.
+ *  - Return value: 0 on success; a positive hipError_t value if a HIP launch failed; or a
+ *    negative LGCN_E* code for invalid arguments (checked on the host before any launch).
+ *    lgcn_error_string() names either kind.
+ *  - Dense embedding blocks are row-major fp32 [rows x d] with leading dimension ld >= d
+ *    (elements). Node ids follow main.py:283-287: users [0,U), items [U,U+I), brands [U+I,N).
+ *  - CSR edge records are 8-byte {int32 col, fp32 val} pairs stored as int64 (lgcn_edge_t),
+ *    rows keep the COO's stored order of their nonzeros (the order torch.sparse.mm sums them in).
+ *  - Numerics: rows of degree <= hub_threshold are summed by one sequential fmaf chain in stored
+ *    order, the exact arithmetic of ATen's addmm_sparse_dense_cpu loop that torch.sparse.mm runs
+ *    on CPU (bitwise identical results). Rows above the threshold ("hubs") are cut into fixed
+ *    chunks summed in a fixed order (deterministic, not bitwise to the CPU order).
+ */
+#ifndef LGCN_H_
+#define LGCN_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGCN_ABI_VERSION 1
+
+/* engine error codes (negative; positive values are hipError_t) */
+#define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
+#define LGCN_EALIGN      (-2)   /* a vectorised path needs 16-B aligned rows; see engine.py */
+#define LGCN_ETOOMANY    (-3)   /* more than LGCN_MAX_LAYERS previous layers in a mean epilogue */
+
+#define LGCN_MAX_LAYERS 16      /* torch.mean over <= 17 stacked layers sums them sequentially */
+
+/* status flags written by lgcn_coo_inspect */
+#define LGCN_COO_ROWS_UNSORTED   1  /* some row index decreases in stored order */
+#define LGCN_COO_OUT_OF_RANGE    2  /* an index is < 0 or >= its dimension */
+#define LGCN_COO_COLS_UNSORTED   4  /* inside a row, columns are not strictly increasing */
+
+/* epilogue modes of lgcn_spmm_layer / lgcn_hub_combine */
+#define LGCN_EPI_STORE 0  /* Y = Â·X */
+#define LGCN_EPI_MEAN  1  /* Y = (((P0 + P1) + ... + P_{n-1}) + Â·X) / div   (lightgcn.py:54) */
+#define LGCN_EPI_ADD   2  /* Y = Z + Â·X                (backward Horner step) */
+
+typedef int64_t lgcn_edge_t;
+
+/* Up to three row segments viewed as one [n x d] block: rows [0,end0) in p0, [end0,end1) in p1,
+ * [end1,n) in p2. This is how E0 = cat(user, item, brand) (lightgcn.py:40) is read without the
+ * copy. A single buffer is {p, p, p, n, n, ld}. */
+typedef struct {
+    const float* p0;
+    const float* p1;
+    const float* p2;
+    int32_t end0;
+    int32_t end1;
+    int64_t ld;
+} lgcn_rows_t;
+
+/* hub work: one chunk of one long row -> one partial-sum slot of d floats */
+typedef struct {
+    int32_t row;
+    int32_t beg;
+    int32_t end;
+    int32_t slot;
+} lgcn_hub_item_t;
+
+/* one long row: its partials occupy slots [first_slot, first_slot + n_slots) */
+typedef struct {
+    int32_t row;
+    int32_t first_slot;
+    int32_t n_slots;
+    int32_t pad;
+} lgcn_hub_row_t;
+
+/* Epilogue operands. prev[0] is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
+ * dense layer buffers E1..E_{n_prev-1} with leading dimension ld_prev. */
+typedef struct {
+    int32_t mode;
+    int32_t n_prev;
+    float div;
+    int32_t pad;
+    lgcn_rows_t prev0;
+    const float* prev_dense[LGCN_MAX_LAYERS];
+    int64_t ld_prev;
+    const float* addend;
+    int64_t ld_add;
+} lgcn_epilogue_t;
+
+/* ---- identification ---------------------------------------------------------------------- */
+int lgcn_abi_version(void);
+const char* lgcn_error_string(int code);
+/* device properties the host side needs (CU count); returns 0/hipError */
+int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host);
+
+/* ---- graph preparation (replaces the per-call COO handling inside torch.sparse.mm) ---------- */
+
+/* Inspect a COO (rows/cols int64, as torch.sparse_coo_tensor._indices()) and OR LGCN_COO_*
+ * flags into *flags (device int32, caller zeroes it). */
+int lgcn_coo_inspect(const int64_t* rows, const int64_t* cols, int64_t nnz, int32_t n_rows,
+                     int32_t n_cols, int32_t* flags, void* stream);
+
+/* Row-sorted COO -> CSR. rowptr[n_rows+1] (int32), edges[nnz]. Order inside a row is kept.
+ * If perm != NULL, input element i is taken from position perm[i] (a stable sort permutation
+ * from lgcn_coo_sort_perm), and row indices are read as keys_sorted[i]. For the transpose of a
+ * non-symmetric Â pass (rows, cols) swapped and the permutation of the stable sort by column. */
+int lgcn_coo_to_csr(const int64_t* rows, const int64_t* cols, const float* vals, int64_t nnz,
+                    int32_t n_rows, const int32_t* perm, const int32_t* keys_sorted,
+                    int32_t* rowptr, lgcn_edge_t* edges, void* stream);
+
+/* Stable sort permutation of nnz keys (int64 in [0, n_keys)) — used for unsorted COO input
+ * (keys = rows) and for the transpose of a non-symmetric Â (keys = cols). Two-call protocol:
+ * with temp == NULL only *temp_bytes_host is written. keys_tmp/keys_sorted/perm_tmp/perm are
+ * caller buffers of nnz int32 each. */
+int lgcn_coo_sort_perm(const int64_t* keys, int64_t nnz, int32_t n_keys, int32_t* keys_tmp,
+                       int32_t* keys_sorted, int32_t* perm_tmp, int32_t* perm, void* temp,
+                       size_t* temp_bytes_host, void* stream);
+
+/* Bitwise symmetry test of a CSR with sorted unique columns: *asym (device int32, zeroed by the
+ * caller) becomes nonzero if some (r,c,v) lacks a bit-identical (c,r,v). When Â is symmetric the
+ * backward Âᵀ·G reuses the forward CSR (torch: SparseAddmmBackward0 computes Âᵀ·G). */
+int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
+                             int64_t nnz, int32_t* asym, void* stream);
+
+/* ---- the propagation (models/lightgcn.py:44-54) -------------------------------------------- */
+
+/* One layer Y = epilogue(Â·X) over rows [0, n_rows):
+ *  - rows with degree <= hub_threshold: one pass, sequential fmaf, epilogue applied in-kernel;
+ *  - hub chunks (n_hub_items, from the host planner) write partials[slot*d ...];
+ *    lgcn_hub_combine then finishes those rows. Both kinds run in ONE launch.
+ * X is read through `x` (segments allowed). Y is [n_rows x ldy]. d in [1, 2048]. */
+int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
+                    int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
+                    float* partials, lgcn_rows_t x, float* y, int64_t ldy, int32_t d,
+                    const lgcn_epilogue_t* epi_host, void* stream);
+
+/* Finish hub rows: sum each row's partial slots in slot order, apply the epilogue, write Y. */
+int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
+                     float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                     void* stream);
+
+/* Y[r,:] = X[r,:] / div for r < n_rows (mean of one layer; backward seed G/(K+1)). */
+int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
+                    void* stream);
+
+/* Whole forward in one call: E1..E_{K-1} into layer_bufs_host[0..K-2] (each [n x d], ld = d),
+ * final = mean(E0..EK) into out [n x d]. emb = E0 segments. Hub plan as in lgcn_spmm_layer
+ * (partials sized for it). ev_host: NULL or 2*K hipEvent_t recorded around each layer's
+ * lgcn_spmm_layer launch (timing only). */
+int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+                           int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
+                           int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
+                           int32_t n_hub_rows, float* partials, lgcn_rows_t emb, int32_t d,
+                           int32_t K, float* const* layer_bufs_host, float* out,
+                           void* const* ev_host, void* stream);
+
+/* Whole backward: grad_e0 = sum_k (Âᵀ)^k G/(K+1) in the Horner order autograd uses
+ * (h = G/(K+1); K times h = G/(K+1) + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric).
+ * work_c, work_h: [n x d] scratch. grad_out/grad_e0 are [n x d] with ld = d. */
+int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
+                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
+                            int32_t n_hub_rows, float* partials, const float* grad_out,
+                            int32_t d, int32_t K, float* work_c, float* work_h, float* grad_e0,
+                            void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LGCN_H_ */

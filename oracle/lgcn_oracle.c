@@ -1,0 +1,81 @@
+/*
+ * lgcn_oracle.c — TEST INFRASTRUCTURE ONLY. CPU restatement of the reference's propagation
+ * arithmetic, used as the parity checker. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product (gcn_recommendation_amd/, models/) never does.
+ *
+ * Pinned against the reference: tests/test_oracle_golden.py checks every function below
+ * bitwise against the golden vectors that tests/golden/gen_golden.py produced by importing the
+ * reference (sha1 of every layer, the final embeddings and the embedding gradients).
+ *
+ * What it restates:
+ *  - torch.sparse.mm(adj_mat, ego) as called at models/lightgcn.py:45: on CPU, ATen's
+ *    addmm_sparse_dense worker zeroes the result, then for every stored nonzero j in stored order
+ *    does r[row_j,:] = fma(val_j, dense[col_j,:], r[row_j,:]) (a cpublas axpy; MKL's saxpy uses
+ *    FMA). Third-party arithmetic: PyTorch (unpinned by the reference; torch 2.10.0 here).
+ *  - torch.mean(torch.stack([E0..EK]), 0) (models/lightgcn.py:54): ((E0+E1)+...+EK)/(K+1),
+ *    sequential, correctly rounded division (holds for K+1 <= 17; checked in tests).
+ *  - The autograd backward of lines 40-54 for an upstream gradient G: MeanBackward gives every
+ *    layer G/(K+1); SparseAddmmBackward0 gives Âᵀ·dE_{k+1}; accumulation is
+ *    dE_k = G/(K+1) + Âᵀ·dE_{k+1} (addition commutes bitwise), i.e. the Horner recurrence.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off; fmaf is the only fused operation).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* Y[n_rows x d] = Â·X for a COO given in stored order (rows/cols int64, vals fp32). */
+void oracle_spmm_coo(int64_t nnz, const int64_t* rows, const int64_t* cols, const float* vals,
+                     int64_t n_rows, int64_t d, const float* x, float* y) {
+    memset(y, 0, sizeof(float) * (size_t)(n_rows * d));
+    for (int64_t j = 0; j < nnz; ++j) {
+        const float v = vals[j];
+        const float* xr = x + cols[j] * d;
+        float* yr = y + rows[j] * d;
+        for (int64_t c = 0; c < d; ++c) yr[c] = fmaf(v, xr[c], yr[c]);
+    }
+}
+
+/* lightgcn.py:40-54 — final[n x d] = mean(E0..EK). layers_out (optional) receives E1..EK
+ * back to back ([K][n][d]). */
+void oracle_forward(int64_t nnz, const int64_t* rows, const int64_t* cols, const float* vals,
+                    int64_t n, int64_t d, int64_t K, const float* e0, float* final_out,
+                    float* layers_out) {
+    const size_t sz = (size_t)(n * d);
+    float* prev = (float*)malloc(sizeof(float) * (sz ? sz : 1));
+    float* cur = (float*)malloc(sizeof(float) * (sz ? sz : 1));
+    memcpy(final_out, e0, sizeof(float) * sz);  /* running sum starts at E0 */
+    memcpy(prev, e0, sizeof(float) * sz);
+    for (int64_t k = 0; k < K; ++k) {
+        oracle_spmm_coo(nnz, rows, cols, vals, n, d, prev, cur);
+        for (size_t i = 0; i < sz; ++i) final_out[i] = final_out[i] + cur[i];
+        if (layers_out) memcpy(layers_out + (size_t)k * sz, cur, sizeof(float) * sz);
+        float* t = prev; prev = cur; cur = t;
+    }
+    const float div = (float)(K + 1);
+    for (size_t i = 0; i < sz; ++i) final_out[i] = final_out[i] / div;
+    free(prev);
+    free(cur);
+}
+
+/* Backward of lightgcn.py:40-54 for upstream G: grad_e0 = dE0. `rows/cols` are Â's COO (the
+ * transpose is taken here, keeping stored order, as torch's sparse t() does). */
+void oracle_backward(int64_t nnz, const int64_t* rows, const int64_t* cols, const float* vals,
+                     int64_t n, int64_t d, int64_t K, const float* g, float* grad_e0) {
+    const size_t sz = (size_t)(n * d);
+    float* c = (float*)malloc(sizeof(float) * (sz ? sz : 1));
+    float* h = (float*)malloc(sizeof(float) * (sz ? sz : 1));
+    float* t = (float*)malloc(sizeof(float) * (sz ? sz : 1));
+    const float div = (float)(K + 1);
+    for (size_t i = 0; i < sz; ++i) c[i] = g[i] / div;
+    memcpy(h, c, sizeof(float) * sz);
+    for (int64_t k = 0; k < K; ++k) {
+        oracle_spmm_coo(nnz, cols, rows, vals, n, d, h, t);  /* Âᵀ·h */
+        for (size_t i = 0; i < sz; ++i) h[i] = c[i] + t[i];
+    }
+    memcpy(grad_e0, h, sizeof(float) * sz);
+    free(c);
+    free(h);
+    free(t);
+}

@@ -1,0 +1,108 @@
+"""The C-ABI library: loads on a CPU host, exports every symbol include/lgcn.h declares, its
+struct layouts match the ctypes mirror, and host-side argument validation answers without
+touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+from gcn_recommendation_amd import _build, engine
+
+HEADER = os.path.join(ROOT, "include", "lgcn.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+(lgcn_\w+)\s*\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    _build.build()
+    return engine.load_library()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 12
+    out = subprocess.check_output(["nm", "-D", "--defined-only", engine.LIB_PATH], text=True)
+    exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    bound = set(name for name, _, _ in engine.ABI)
+    assert set(syms) == bound, set(syms) ^ bound
+
+
+def test_library_is_gfx950_code_object(lib):
+    blob = open(engine.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_version_and_errors(lib):
+    assert lib.lgcn_abi_version() == 1
+    assert b"invalid" in lib.lgcn_error_string(-1)
+    assert lib.lgcn_error_string(0) == b"success"
+
+
+def test_argument_validation_without_gpu(lib):
+    ep = engine.EpilogueT()
+    ep.mode = 7
+    rows = engine.RowsT()
+    # bad epilogue / bad d / negative sizes return before any HIP call
+    assert lib.lgcn_spmm_layer(None, None, 0, 0, None, 0, None, rows, None, 0, 64,
+                               ctypes.byref(ep), None) == -1
+    ep.mode = engine.LGCN_EPI_STORE
+    assert lib.lgcn_spmm_layer(None, None, 10, 0, None, 0, None, rows, None, 0, 0,
+                               ctypes.byref(ep), None) == -1
+    assert lib.lgcn_spmm_layer(None, None, -1, 0, None, 0, None, rows, None, 0, 64,
+                               ctypes.byref(ep), None) == -1
+    ep.mode = engine.LGCN_EPI_MEAN
+    ep.n_prev = 18
+    ep.div = 2.0
+    assert lib.lgcn_hub_combine(None, 0, None, None, 64, 64, ctypes.byref(ep), None) == -3
+    assert lib.lgcn_propagate_forward(None, None, 5, 0, None, 0, None, 0, None, rows, 64, -1,
+                                      None, None, None, None) == -1
+    nbytes = ctypes.c_size_t(0)
+    assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
+                                  ctypes.byref(nbytes), None) == -1
+
+
+def test_struct_layout_matches_header():
+    """Compile a probe against include/lgcn.h with gcc and compare sizeof/offsetof."""
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "lgcn.h"
+int main(void){
+ printf("%zu %zu %zu %zu\n", sizeof(lgcn_rows_t), sizeof(lgcn_epilogue_t),
+        sizeof(lgcn_hub_item_t), sizeof(lgcn_hub_row_t));
+ printf("%zu %zu %zu %zu %zu\n", offsetof(lgcn_epilogue_t, prev0),
+        offsetof(lgcn_epilogue_t, prev_dense), offsetof(lgcn_epilogue_t, ld_prev),
+        offsetof(lgcn_epilogue_t, addend), offsetof(lgcn_epilogue_t, ld_add));
+ return 0;}
+"""
+    with tempfile.TemporaryDirectory() as td:
+        c = os.path.join(td, "probe.c")
+        exe = os.path.join(td, "probe")
+        open(c, "w").write(src)
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        l1, l2 = subprocess.check_output([exe], text=True).split("\n")[:2]
+    sizes = [int(x) for x in l1.split()]
+    offs = [int(x) for x in l2.split()]
+    assert sizes == [ctypes.sizeof(engine.RowsT), ctypes.sizeof(engine.EpilogueT), 16, 16]
+    E = engine.EpilogueT
+    assert offs == [E.prev0.offset, E.prev_dense.offset, E.ld_prev.offset, E.addend.offset,
+                    E.ld_add.offset]
+
+
+def test_engine_refuses_missing_library(tmp_path):
+    with pytest.raises(engine.LgcnError):
+        engine._lib, saved = None, engine._lib
+        try:
+            engine.load_library(str(tmp_path / "nope.so"))
+        finally:
+            engine._lib = saved

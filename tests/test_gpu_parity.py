@@ -1,0 +1,254 @@
+"""GPU parity of the HIP engine (through the C ABI) against the golden vectors and the oracle.
+
+Bar: bitwise wherever the engine runs the reference's sequential order (every row with degree
+<= hub threshold; all rows under LGCN_HUB_THRESHOLD=exact); otherwise, for chunked hub rows,
+the north_star tolerance max|got-ref| <= 1e-5 * max|ref| per tensor."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import CASES, Cfg, case_dims, case_e0, load_case, upstream_grad
+from gcn_recommendation_amd import engine, graph
+from gcn_recommendation_amd.loss import bpr_loss_reg
+from models.lightgcn import LightGCN
+from models.lightgcn_fusion import LightGCN_Fusion
+from oracle import oracle
+from util import assert_close_normwise, sha1
+
+pytestmark = pytest.mark.gpu
+
+
+def _adj(z, dev):
+    U, I, B, d, K = case_dims(z)
+    return graph.build_norm_adj(z["train_user"], z["train_item"], U, I, B, z["ib_item"],
+                                z["ib_brand"], bool(z["use_brand"]), device=dev)
+
+
+def _model(z, dev, fusion=False):
+    U, I, B, d, K = case_dims(z)
+    torch.manual_seed(42)
+    if fusion:
+        return LightGCN_Fusion(U, I, B, Cfg(d, K), pretrained_item_emb=z["content"]).to(dev)
+    return LightGCN(U, I, B, Cfg(d, K)).to(dev)
+
+
+@pytest.mark.parametrize("mode", ["exact", "default"])
+@pytest.mark.parametrize("name", CASES)
+def test_model_forward_backward_vs_reference(gpu_device, monkeypatch, name, mode):
+    if mode == "exact":
+        monkeypatch.setenv("LGCN_HUB_THRESHOLD", "exact")
+    z = load_case(name)
+    U, I, B, d, K = case_dims(z)
+    m = _model(z, gpu_device)
+    adj = _adj(z, gpu_device)
+    fu, fi, fb, u0, i0 = m(adj, use_brand=bool(z["use_brand"]))
+    final = torch.cat([fu, fi, fb])
+    G = torch.from_numpy(upstream_grad(U + I + B, d)).to(gpu_device)
+    (final * G).sum().backward()
+    got = final.detach().cpu().numpy()
+    grads = {n: p.grad.cpu().numpy() for n, p in m.named_parameters()}
+    graph_ = engine.graph_from_coo(adj)
+    has_hubs = graph_.degrees().max(initial=0) > engine.hub_threshold_from_env()
+    if not has_hubs:
+        assert sha1(got) == str(z["sha1/final"]), "forward not bitwise"
+        for n, g in grads.items():
+            assert sha1(g) == str(z["sha1/grad/" + n]), f"grad {n} not bitwise"
+    else:
+        r, c, v = z["adj_row"], z["adj_col"], z["adj_val"]
+        assert_close_normwise(got, oracle.forward(r, c, v, case_e0(z), K), what="final")
+        g0 = oracle.backward(r, c, v, upstream_grad(U + I + B, d), K)
+        assert_close_normwise(grads["user_embedding.weight"], g0[:U], what="grad user")
+        assert_close_normwise(grads["item_embedding.weight"], g0[U:U + I], what="grad item")
+    assert graph_.symmetric
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_recall_ndcg_identical(gpu_device, name):
+    """Recall@K / NDCG@K (main.py:404-439) from GPU embeddings == the reference's numbers."""
+    z = load_case(name)
+    U, I, B, d, K = case_dims(z)
+    m = _model(z, gpu_device)
+    with torch.no_grad():
+        fu, fi, _, _, _ = m(_adj(z, gpu_device))
+    rec, ndcg = oracle.evaluate(fu.cpu().numpy(), fi.cpu().numpy(), z["val_user"], z["val_item"],
+                                z["train_user"], z["train_item"], int(z["eval_k"]))
+    assert rec == float(z["recall"]) and ndcg == float(z["ndcg"])
+
+
+def test_bpr_training_step_matches_reference(gpu_device):
+    z = load_case("c1_brand")
+    m = _model(z, gpu_device)
+    adj = _adj(z, gpu_device)
+    bu, bp, bn = (torch.from_numpy(z[k]).to(gpu_device) for k in ("bpr_users", "bpr_pos",
+                                                                  "bpr_neg"))
+    fu, fi, fb, u0, i0 = m(adj, use_brand=True)
+    loss = bpr_loss_reg(fu[bu], fi[bp], fi[bn], u0[bu], i0[bp], i0[bn], 1e-4,
+                        final_brand_emb=fb)
+    loss.backward()
+    assert abs(loss.item() - float(z["bpr_loss"])) <= 1e-6 * abs(float(z["bpr_loss"]))
+    for n, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy()[:4], z["head/bpr_grad/" + n],
+                                   rtol=1e-5, atol=1e-5 * float(z["absmax/bpr_grad/" + n]))
+
+
+def test_fusion_model_vs_reference(gpu_device):
+    """LightGCN_Fusion: the Linear runs on hipBLASLt (not bitwise to MKL); the propagation of
+    its output is checked bitwise against the oracle on the same E0, and the final embeddings
+    within 1e-5 of the reference's."""
+    z = load_case("c1_fusion")
+    U, I, B, d, K = case_dims(z)
+    m = _model(z, gpu_device, fusion=True)
+    adj = _adj(z, gpu_device)
+    fu, fi, fb, u0, i0 = m(adj)
+    final = torch.cat([fu, fi, fb]).detach().cpu().numpy()
+    assert_close_normwise(final, z["full/final"], what="fusion final")
+    with torch.no_grad():
+        e0 = torch.cat([m.user_embedding.weight, m.fused_item_embedding(),
+                        m.brand_embedding.weight]).cpu().numpy()
+    want = oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], e0, K)
+    assert np.array_equal(final, want)
+    (torch.cat([fu, fi, fb]).sum()).backward()
+    assert m.item_fusion_layer.weight.grad is not None
+
+
+def _rand_graph(n, nnz, seed, symmetric=True):
+    rng = np.random.default_rng(seed)
+    r = rng.integers(0, n, nnz)
+    c = rng.integers(0, n, nnz)
+    if symmetric:
+        r, c = np.concatenate([r, c]), np.concatenate([c, r])
+    key = np.unique(r * n + c)
+    r, c = key // n, key % n
+    v = rng.standard_normal(len(r)).astype(np.float32)
+    if symmetric:
+        lo = np.minimum(r, c) * n + np.maximum(r, c)
+        _, inv = np.unique(lo, return_inverse=True)
+        v = rng.standard_normal(inv.max() + 1).astype(np.float32)[inv]
+    return r, c, v
+
+
+@pytest.mark.parametrize("d", [1, 3, 4, 12, 16, 32, 64, 100, 128, 256, 512])
+def test_dims_and_layers_bitwise(gpu_device, d):
+    n = 700
+    r, c, v = _rand_graph(n, 5000, d)
+    for K in (0, 1, 3):
+        e0 = np.random.default_rng(d + K).standard_normal((n, d)).astype(np.float32)
+        adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
+                                      (n, n)).to(gpu_device)
+        got = engine.propagate_forward(engine.graph_from_coo(adj),
+                                       [torch.from_numpy(e0).to(gpu_device)], K).cpu().numpy()
+        assert np.array_equal(got, oracle.forward(r, c, v, e0, K)), (d, K)
+
+
+def test_segments_and_misaligned_rows(gpu_device):
+    """E0 as three segments with unaligned bases (scalar path) == contiguous E0."""
+    n1, n2, n3, d = 300, 200, 50, 64
+    n = n1 + n2 + n3
+    r, c, v = _rand_graph(n, 4000, 5)
+    e0 = np.random.default_rng(1).standard_normal((n, d)).astype(np.float32)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
+                                  (n, n)).to(gpu_device)
+    gr = engine.graph_from_coo(adj)
+    want = oracle.forward(r, c, v, e0, 3)
+    t = torch.from_numpy(e0).to(gpu_device)
+    segs = [t[:n1].clone(), t[n1:n1 + n2].clone(), t[n1 + n2:].clone()]
+    assert np.array_equal(engine.propagate_forward(gr, segs, 3).cpu().numpy(), want)
+    big = torch.empty(n * d + 1, device=gpu_device)
+    big[1:] = t.reshape(-1)
+    mis = big[1:].view(n, d)  # 4-byte offset: not 16-B aligned
+    assert mis.data_ptr() % 16 != 0
+    assert np.array_equal(engine.propagate_forward(gr, [mis], 3).cpu().numpy(), want)
+
+
+def test_unsorted_coo_with_duplicates(gpu_device):
+    """Arbitrary stored order + duplicate coordinates: the stable sort keeps torch's per-row
+    order, so results stay bitwise = torch.sparse.mm on that COO (oracle)."""
+    rng = np.random.default_rng(2)
+    n, nnz, d = 900, 20000, 64
+    r = rng.integers(0, n, nnz)
+    c = rng.integers(0, n, nnz)
+    v = rng.standard_normal(nnz).astype(np.float32)
+    e0 = rng.standard_normal((n, d)).astype(np.float32)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
+                                  (n, n)).to(gpu_device)
+    g = engine.graph_from_coo(adj)
+    assert not g.symmetric
+    got = engine.propagate_forward(g, [torch.from_numpy(e0).to(gpu_device)], 2,
+                                   hub_threshold=engine.INT32_MAX).cpu().numpy()
+    assert np.array_equal(got, oracle.forward(r, c, v, e0, 2))
+    G = rng.standard_normal((n, d)).astype(np.float32)
+    gb = engine.propagate_backward(g, torch.from_numpy(G).to(gpu_device), 2,
+                                   hub_threshold=engine.INT32_MAX).cpu().numpy()
+    assert np.array_equal(gb, oracle.backward(r, c, v, G, 2))
+
+
+def test_hub_rows_chunked_vs_exact(gpu_device):
+    """A 20k-edge hub row: chunked (default) within tolerance, exact mode bitwise; both
+    deterministic run to run."""
+    rng = np.random.default_rng(3)
+    n, d = 30000, 64
+    hub_c = rng.permutation(n)[:20000]
+    r = np.concatenate([np.zeros(20000, np.int64), rng.integers(1, n, 40000)])
+    c = np.concatenate([hub_c, rng.integers(0, n, 40000)])
+    r, c = np.concatenate([r, c]), np.concatenate([c, r])
+    key = np.unique(r * n + c)
+    r, c = key // n, key % n
+    v = (rng.random(len(r)).astype(np.float32) * 0.01)
+    e0 = rng.standard_normal((n, d)).astype(np.float32)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
+                                  (n, n)).to(gpu_device)
+    g = engine.graph_from_coo(adj)
+    x = [torch.from_numpy(e0).to(gpu_device)]
+    want = oracle.forward(r, c, v, e0, 3)
+    exact = engine.propagate_forward(g, x, 3, hub_threshold=engine.INT32_MAX).cpu().numpy()
+    assert np.array_equal(exact, want)
+    a = engine.propagate_forward(g, x, 3, hub_threshold=256).cpu().numpy()
+    b = engine.propagate_forward(g, x, 3, hub_threshold=256).cpu().numpy()
+    assert np.array_equal(a, b)
+    assert_close_normwise(a, want, what="chunked hub")
+    assert g.hubs(256).n_rows >= 1
+
+
+def test_empty_graph_and_isolated_rows(gpu_device):
+    n, d = 10, 16
+    adj = torch.sparse_coo_tensor(torch.zeros((2, 0), dtype=torch.int64), torch.zeros(0),
+                                  (n, n)).to(gpu_device)
+    e0 = torch.randn(n, d, device=gpu_device)
+    out = engine.propagate_forward(engine.graph_from_coo(adj), [e0], 3)
+    assert torch.equal(out, (e0 + 0 + 0 + 0) / 4)
+
+
+def test_plan_cache_reused_and_invalidated(gpu_device):
+    z = load_case("micro_d12")
+    adj = _adj(z, gpu_device)
+    g1 = engine.graph_from_coo(adj)
+    assert engine.graph_from_coo(adj) is g1
+    adj._values().mul_(1.0)  # bumps the version counter
+    assert engine.graph_from_coo(adj) is not g1
+
+
+def test_c2_scale_uniform_and_powerlaw(gpu_device):
+    """BASELINE configs[1] shapes (50k x 50k, 1M interactions, d=64, K=3): exact mode bitwise,
+    default mode within tolerance, forward and backward."""
+    for gen in ("uniform", "powerlaw"):
+        if gen == "uniform":
+            u, i = graph.uniform_interactions(50_000, 50_000, 1_000_000, 1)
+        else:
+            u, i = graph.powerlaw_interactions(50_000, 50_000, 1_000_000, 2)
+        U, I = 50_000, 50_000
+        rows, cols = graph.edge_lists(u, i, U, I, use_brand=False)
+        r, c, v = graph.normalise(rows, cols, U + I)
+        adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
+                                      (U + I, U + I)).to(gpu_device)
+        g = engine.graph_from_coo(adj)
+        assert g.symmetric
+        e0 = np.random.default_rng(0).standard_normal((U + I, 64)).astype(np.float32) * 0.01
+        x = [torch.from_numpy(e0).to(gpu_device)]
+        want = oracle.forward(r, c, v, e0, 3)
+        exact = engine.propagate_forward(g, x, 3, hub_threshold=engine.INT32_MAX)
+        assert np.array_equal(exact.cpu().numpy(), want), gen
+        fast = engine.propagate_forward(g, x, 3).cpu().numpy()
+        assert_close_normwise(fast, want, what=gen)
+        G = np.random.default_rng(1).standard_normal((U + I, 64)).astype(np.float32)
+        gb = engine.propagate_backward(g, torch.from_numpy(G).to(gpu_device), 3).cpu().numpy()
+        assert_close_normwise(gb, oracle.backward(r, c, v, G, 3), what=gen + " bwd")
