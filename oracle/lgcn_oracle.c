@@ -79,3 +79,38 @@ void oracle_backward(int64_t nnz, const int64_t* rows, const int64_t* cols, cons
     free(h);
     free(t);
 }
+
+/* fp64 arbiter (not a restatement): the same propagation in double precision over a row-sorted
+ * COO, OpenMP over rows. Used to measure how far the fp32 reference AND the engine are from
+ * exact arithmetic on graphs whose hub rows make the reference's own rounding error exceed the
+ * 1e-5 normwise gate (bench.py parity fields, tests/test_gpu_parity.py). */
+void oracle_forward_f64(int64_t nnz, const int64_t* rows, const int64_t* cols, const float* vals,
+                        int64_t n, int64_t d, int64_t K, const float* e0, double* final_out) {
+    const size_t sz = (size_t)(n * d);
+    int64_t* rowptr = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    for (int64_t j = 0; j < nnz; ++j) rowptr[rows[j] + 1]++;
+    for (int64_t r = 0; r < n; ++r) rowptr[r + 1] += rowptr[r];
+    double* prev = (double*)malloc(sizeof(double) * (sz ? sz : 1));
+    double* cur = (double*)malloc(sizeof(double) * (sz ? sz : 1));
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)sz; ++i) { prev[i] = e0[i]; final_out[i] = e0[i]; }
+    for (int64_t k = 0; k < K; ++k) {
+#pragma omp parallel for schedule(dynamic, 1024)
+        for (int64_t r = 0; r < n; ++r) {
+            double* yr = cur + r * d;
+            for (int64_t c = 0; c < d; ++c) yr[c] = 0.0;
+            for (int64_t j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+                const double v = vals[j];
+                const double* xr = prev + cols[j] * d;
+                for (int64_t c = 0; c < d; ++c) yr[c] += v * xr[c];
+            }
+            for (int64_t c = 0; c < d; ++c) final_out[r * d + c] += yr[c];
+        }
+        double* t = prev; prev = cur; cur = t;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)sz; ++i) final_out[i] /= (double)(K + 1);
+    free(rowptr);
+    free(prev);
+    free(cur);
+}

@@ -48,7 +48,9 @@ def _load():
     lib.oracle_spmm_coo.argtypes = [i64, p, p, p, i64, i64, p, p]
     lib.oracle_forward.argtypes = [i64, p, p, p, i64, i64, i64, p, p, p]
     lib.oracle_backward.argtypes = [i64, p, p, p, i64, i64, i64, p, p]
-    for f in (lib.oracle_spmm_coo, lib.oracle_forward, lib.oracle_backward):
+    lib.oracle_forward_f64.argtypes = [i64, p, p, p, i64, i64, i64, p, p]
+    for f in (lib.oracle_spmm_coo, lib.oracle_forward, lib.oracle_backward,
+              lib.oracle_forward_f64):
         f.restype = None
     _lib = lib
     return lib
@@ -131,6 +133,17 @@ def backward(rows, cols, vals, g, K):
     out = np.empty_like(g)
     _load().oracle_backward(len(vals), _ptr(rows), _ptr(cols), _ptr(vals), n, d, K, _ptr(g),
                             _ptr(out))
+    return out
+
+
+def forward_f64(rows, cols, vals, e0, K):
+    """fp64 arbiter of the forward (row-sorted COO): exact-arithmetic yardstick, not a restatement."""
+    rows, cols, vals = _coo(rows, cols, vals)
+    e0 = np.ascontiguousarray(e0, dtype=np.float32)
+    n, d = e0.shape
+    out = np.empty((n, d), np.float64)
+    _load().oracle_forward_f64(len(vals), _ptr(rows), _ptr(cols), _ptr(vals), n, d, K, _ptr(e0),
+                               _ptr(out))
     return out
 
 

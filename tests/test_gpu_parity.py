@@ -59,7 +59,7 @@ def test_model_forward_backward_vs_reference(gpu_device, monkeypatch, name, mode
         g0 = oracle.backward(r, c, v, upstream_grad(U + I + B, d), K)
         assert_close_normwise(grads["user_embedding.weight"], g0[:U], what="grad user")
         assert_close_normwise(grads["item_embedding.weight"], g0[U:U + I], what="grad item")
-    assert graph_.symmetric
+    assert graph_.transpose is not None
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -241,7 +241,9 @@ def test_c2_scale_uniform_and_powerlaw(gpu_device):
         adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
                                       (U + I, U + I)).to(gpu_device)
         g = engine.graph_from_coo(adj)
-        assert g.symmetric
+        # duplicate multiplicities m >= 3 make fp32 (d_r*m)*d_c != (d_c*m)*d_r: Â is then not
+        # bitwise symmetric and the backward must run on the transpose CSR
+        assert g.transpose is not None
         e0 = np.random.default_rng(0).standard_normal((U + I, 64)).astype(np.float32) * 0.01
         x = [torch.from_numpy(e0).to(gpu_device)]
         want = oracle.forward(r, c, v, e0, 3)
