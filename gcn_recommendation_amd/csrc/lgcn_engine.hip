@@ -128,7 +128,85 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
     }
 }
 
-template <typename V, int G, int NV, int MODE>
+// Rows of one group, RPG at a time: the group walks the bundle's edges as ONE stream (hub rows
+// skipped), keeps U gathers in flight across row boundaries, and folds them in stored order,
+// flushing a row's accumulator (fused epilogue) when the stream passes its end. Each row is still
+// one sequential fmaf chain, so results are identical to RPG = 1; what changes is how many
+// gathers are in flight per group and how many dependent rowptr->edge->gather chains a row pays.
+template <typename V, int G, int NV, int MODE, int RPG, int U>
+__device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
+                                            const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
+                                            int32_t hub_thr, int32_t r0, const lgcn_rows_t& x,
+                                            float* __restrict__ y, int64_t ldy, int lane, int dW,
+                                            const lgcn_epilogue_t& ep) {
+    using T = VT<V>;
+    static_assert(RPG < G || G == 64, "row boundaries are held one per lane");
+    const int nrows = min(RPG, n_rows - r0);
+    // lane l (l <= nrows) holds rowptr[r0 + l]; boundaries are read back by shuffles
+    const int32_t rpl = (lane <= nrows) ? rowptr[r0 + lane] : 0;
+    auto bnd = [&](int i) { return __shfl(rpl, i, G); };
+    V acc[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) acc[q] = T::zero();
+    int fr = 0;                              // next row to flush (bundle-relative)
+    int lr = 0;                              // row the load cursor is in
+    int32_t lend = bnd(1);
+    int32_t j = bnd(0);
+    if (lend - j > hub_thr) j = lend;        // hub rows: edges owned by the chunk path
+    auto flush = [&](int i) {
+        const int32_t deg = bnd(i + 1) - bnd(i);
+        if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, r0 + i, lane, dW, acc, y, ldy);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) acc[q] = T::zero();
+    };
+    while (true) {
+        int2 e[U];
+        int rid[U];
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            while (j >= lend && lr < nrows) {
+                ++lr;
+                if (lr < nrows) {
+                    const int32_t b = bnd(lr);
+                    lend = bnd(lr + 1);
+                    j = (lend - b > hub_thr) ? lend : b;
+                }
+            }
+            rid[u] = lr;
+            if (lr < nrows) {
+                e[u] = load_edge(edges + j);
+                ++j;
+                ++cnt;
+            } else {
+                e[u] = make_int2(0, 0);
+            }
+        }
+        V xv[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float* rp = seg_row(x, e[u].x);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int c = lane + q * G;
+                xv[u][q] = (u < cnt && c < dW) ? T::load(rp + c * T::W) : T::zero();
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u < cnt) {
+                while (fr < rid[u]) flush(fr++);
+                const float v = __int_as_float(e[u].y);
+#pragma unroll
+                for (int q = 0; q < NV; ++q) acc[q] = T::fma(v, xv[u][q], acc[q]);
+            }
+        }
+        if (cnt < U) break;
+    }
+    while (fr < nrows) flush(fr++);
+}
+
+template <typename V, int G, int NV, int MODE, int RPG, int U>
 __global__ __launch_bounds__(kBlock) void k_layer(
     const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
     int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
@@ -136,17 +214,16 @@ __global__ __launch_bounds__(kBlock) void k_layer(
     int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep) {
     using T = VT<V>;
     constexpr int RPB = kBlock / G;
-    constexpr int U = NV >= 8 ? 1 : 8 / NV;
     const int lane = threadIdx.x & (G - 1);
     const int grp = threadIdx.x / G;
-    V acc[NV];
-#pragma unroll
-    for (int q = 0; q < NV; ++q) acc[q] = T::zero();
 
     if ((int32_t)blockIdx.x < hub_blocks) {  // hub chunks first: the longest work starts earliest
         const int32_t it = blockIdx.x * RPB + grp;
         if (it >= n_items) return;
         const lgcn_hub_item_t w = items[it];
+        V acc[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) acc[q] = T::zero();
         accumulate<V, G, NV, U>(edges, w.beg, w.end, x, lane, dW, acc);
         float* pr = partials + (int64_t)w.slot * d;
 #pragma unroll
@@ -156,13 +233,24 @@ __global__ __launch_bounds__(kBlock) void k_layer(
         }
         return;
     }
-    const int32_t row = (int32_t)(blockIdx.x - hub_blocks) * RPB + grp;
-    if (row >= n_rows) return;
-    const int32_t beg = rowptr[row];
-    const int32_t end = rowptr[row + 1];
-    if (end - beg > hub_thr) return;  // owned by the hub chunks + k_hub_combine
-    accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
-    epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
+    const int64_t gidx = (int64_t)(blockIdx.x - hub_blocks) * RPB + grp;
+    if constexpr (RPG == 1) {
+        const int32_t row = (int32_t)gidx;
+        if (gidx >= n_rows) return;
+        const int32_t beg = rowptr[row];
+        const int32_t end = rowptr[row + 1];
+        if (end - beg > hub_thr) return;  // owned by the hub chunks + k_hub_combine
+        V acc[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) acc[q] = T::zero();
+        accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
+        epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
+    } else {
+        const int64_t r0 = gidx * RPG;
+        if (r0 >= n_rows) return;
+        rows_bundle<V, G, NV, MODE, RPG, U>(rowptr, edges, n_rows, hub_thr, (int32_t)r0, x, y, ldy,
+                                            lane, dW, ep);
+    }
 }
 
 // One block per hub row: group g sums slots g, g+NG, ... in order; groups are then added in
@@ -181,13 +269,24 @@ __global__ __launch_bounds__(kBlock) void k_hub_combine(const lgcn_hub_row_t* __
     V acc[NV];
 #pragma unroll
     for (int q = 0; q < NV; ++q) acc[q] = T::zero();
-    for (int s = grp; s < hr.n_slots; s += NG) {
-        const float* pr = partials + (int64_t)(hr.first_slot + s) * d;
+    constexpr int UC = 8;  // slot loads in flight per group; added in slot order
+    for (int s0 = grp; s0 < hr.n_slots; s0 += NG * UC) {
+        V pv[UC][NV];
 #pragma unroll
-        for (int q = 0; q < NV; ++q) {
-            const int c = lane + q * G;
-            if (c < dW) acc[q] = T::add(acc[q], T::load(pr + c * T::W));
+        for (int u = 0; u < UC; ++u) {
+            const int s = s0 + u * NG;
+            const float* pr = partials + (int64_t)(hr.first_slot + s) * d;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int c = lane + q * G;
+                pv[u][q] = (s < hr.n_slots && c < dW) ? T::load(pr + c * T::W) : T::zero();
+            }
         }
+#pragma unroll
+        for (int u = 0; u < UC; ++u)
+            if (s0 + u * NG < hr.n_slots)
+#pragma unroll
+                for (int q = 0; q < NV; ++q) acc[q] = T::add(acc[q], pv[u][q]);
     }
 #pragma unroll
     for (int q = 0; q < NV; ++q) red[grp][lane + q * G] = acc[q];
@@ -342,37 +441,65 @@ bool epi_aligned(const lgcn_epilogue_t& ep) {
     return true;
 }
 
-template <typename V, int G, int NV>
-int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
-                   const lgcn_hub_item_t* items, int32_t n_items, float* partials,
-                   const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
-                   const lgcn_epilogue_t& ep, hipStream_t s) {
+// tuning knobs (lgcn_tune): rows per lane group and gathers in flight per group (d = 64 only)
+int g_rows_per_group = 8;
+int g_unroll = 8;
+
+template <typename V, int G, int NV, int RPG, int U>
+int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+                     const lgcn_hub_item_t* items, int32_t n_items, float* partials,
+                     const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
+                     const lgcn_epilogue_t& ep, hipStream_t s) {
     constexpr int RPB = kBlock / G;
     const int32_t hub_blocks = (n_items + RPB - 1) / RPB;
-    const int64_t row_blocks = ((int64_t)n_rows + RPB - 1) / RPB;
+    const int64_t row_groups = ((int64_t)n_rows + RPG - 1) / RPG;
+    const int64_t row_blocks = (row_groups + RPB - 1) / RPB;
     const int64_t grid = hub_blocks + row_blocks;
     if (grid == 0) return 0;
     if (grid > 0x7fffffffLL) return LGCN_EINVAL;
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_STORE>), dim3((uint32_t)grid), dim3(kBlock),
-                               0, s, rowptr, edges, n_rows, thr, items, n_items, hub_blocks,
-                               partials, x, y, ldy, d, dW, ep);
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_STORE, RPG, U>), dim3((uint32_t)grid),
+                               dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                               hub_blocks, partials, x, y, ldy, d, dW, ep);
             break;
         case LGCN_EPI_MEAN:
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN>), dim3((uint32_t)grid), dim3(kBlock),
-                               0, s, rowptr, edges, n_rows, thr, items, n_items, hub_blocks,
-                               partials, x, y, ldy, d, dW, ep);
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN, RPG, U>), dim3((uint32_t)grid),
+                               dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                               hub_blocks, partials, x, y, ldy, d, dW, ep);
             break;
         case LGCN_EPI_ADD:
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD>), dim3((uint32_t)grid), dim3(kBlock),
-                               0, s, rowptr, edges, n_rows, thr, items, n_items, hub_blocks,
-                               partials, x, y, ldy, d, dW, ep);
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U>), dim3((uint32_t)grid),
+                               dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                               hub_blocks, partials, x, y, ldy, d, dW, ep);
             break;
         default:
             return LGCN_EINVAL;
     }
     return last_err();
+}
+
+template <typename V, int G, int NV>
+int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+                   const lgcn_hub_item_t* items, int32_t n_items, float* partials,
+                   const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
+                   const lgcn_epilogue_t& ep, hipStream_t s) {
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    constexpr int RPG_MAX = G > 8 ? 8 : G - 1;  // boundaries live one per lane of the group
+    if (g_rows_per_group <= 1 || RPG_MAX <= 1)
+        return launch_layer_rpg<V, G, NV, 1, U>(rowptr, edges, n_rows, thr, items, n_items,
+                                                partials, x, y, ldy, d, dW, ep, s);
+    if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: extra variants for tuning
+#define LGCN_V(R_, U_)                                                                          \
+    if (g_rows_per_group == R_ && g_unroll == U_)                                              \
+        return launch_layer_rpg<V, G, NV, R_, U_>(rowptr, edges, n_rows, thr, items, n_items,  \
+                                                  partials, x, y, ldy, d, dW, ep, s);
+        LGCN_V(2, 8) LGCN_V(4, 8) LGCN_V(15, 8) LGCN_V(4, 4) LGCN_V(8, 4) LGCN_V(15, 4)
+        LGCN_V(8, 6) LGCN_V(8, 12)
+#undef LGCN_V
+    }
+    return launch_layer_rpg<V, G, NV, RPG_MAX, U>(rowptr, edges, n_rows, thr, items, n_items,
+                                                  partials, x, y, ldy, d, dW, ep, s);
 }
 
 template <typename V, int G, int NV>
@@ -525,6 +652,23 @@ int valid_geom(int32_t n_rows, int32_t d) {
 extern "C" {
 
 int lgcn_abi_version(void) { return LGCN_ABI_VERSION; }
+
+int lgcn_tune(int knob, int value) {
+    switch (knob) {
+        case LGCN_TUNE_ROWS_PER_GROUP: {
+            const int old = g_rows_per_group;
+            if (value > 0) g_rows_per_group = value;
+            return old;
+        }
+        case LGCN_TUNE_UNROLL: {
+            const int old = g_unroll;
+            if (value > 0) g_unroll = value;
+            return old;
+        }
+        default:
+            return LGCN_EINVAL;
+    }
+}
 
 const char* lgcn_error_string(int code) {
     switch (code) {

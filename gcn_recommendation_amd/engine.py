@@ -23,6 +23,7 @@ LGCN_EPI_STORE, LGCN_EPI_MEAN, LGCN_EPI_ADD = 0, 1, 2
 LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
+TUNE_ROWS_PER_GROUP, TUNE_UNROLL = 1, 2
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
@@ -54,6 +55,7 @@ _P, _I32, _I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
 ABI = [
     ("lgcn_abi_version", ctypes.c_int, []),
     ("lgcn_error_string", ctypes.c_char_p, [ctypes.c_int]),
+    ("lgcn_tune", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("lgcn_device_info", ctypes.c_int, [ctypes.c_int, _P, _P]),
     ("lgcn_coo_inspect", ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
     ("lgcn_coo_to_csr", ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P]),

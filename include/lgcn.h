@@ -103,6 +103,12 @@ typedef struct {
 /* ---- identification ---------------------------------------------------------------------- */
 int lgcn_abi_version(void);
 const char* lgcn_error_string(int code);
+/* Tuning knobs (process-global; not needed for correctness — results do not depend on them).
+ * Returns the previous value (value <= 0 only queries), or LGCN_EINVAL for an unknown knob. */
+#define LGCN_TUNE_ROWS_PER_GROUP 1  /* rows streamed by one lane group in k_layer (default 8) */
+#define LGCN_TUNE_UNROLL         2  /* gathers in flight per lane group, d = 64 (default 8) */
+int lgcn_tune(int knob, int value);
+
 /* device properties the host side needs (CU count); returns 0/hipError */
 int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host);
 
