@@ -224,7 +224,8 @@ __global__ __launch_bounds__(kBlock) void k_layer(
         V acc[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
-        accumulate<V, G, NV, U>(edges, w.beg, w.end, x, lane, dW, acc);
+        constexpr int UH = NV >= 8 ? 1 : 8 / NV;  // hub chunks are long: deep unroll
+        accumulate<V, G, NV, UH>(edges, w.beg, w.end, x, lane, dW, acc);
         float* pr = partials + (int64_t)w.slot * d;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -441,9 +442,10 @@ bool epi_aligned(const lgcn_epilogue_t& ep) {
     return true;
 }
 
-// tuning knobs (lgcn_tune): rows per lane group and gathers in flight per group (d = 64 only)
-int g_rows_per_group = 8;
-int g_unroll = 8;
+// tuning knobs (lgcn_tune): 0 = automatic choice; explicit (rows per group, gathers in flight)
+// pairs select a fixed d = 64 variant for A/B timing
+int g_rows_per_group = 0;
+int g_unroll = 0;
 
 template <typename V, int G, int NV, int RPG, int U>
 int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
@@ -484,22 +486,23 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_ro
                    const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                    const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
                    const lgcn_epilogue_t& ep, hipStream_t s) {
-    constexpr int U = NV >= 8 ? 1 : 8 / NV;
-    constexpr int RPG_MAX = G > 8 ? 8 : G - 1;  // boundaries live one per lane of the group
-    if (g_rows_per_group <= 1 || RPG_MAX <= 1)
-        return launch_layer_rpg<V, G, NV, 1, U>(rowptr, edges, n_rows, thr, items, n_items,
-                                                partials, x, y, ldy, d, dW, ep, s);
-    if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: extra variants for tuning
-#define LGCN_V(R_, U_)                                                                          \
-    if (g_rows_per_group == R_ && g_unroll == U_)                                              \
-        return launch_layer_rpg<V, G, NV, R_, U_>(rowptr, edges, n_rows, thr, items, n_items,  \
-                                                  partials, x, y, ldy, d, dW, ep, s);
-        LGCN_V(2, 8) LGCN_V(4, 8) LGCN_V(15, 8) LGCN_V(4, 4) LGCN_V(8, 4) LGCN_V(15, 4)
-        LGCN_V(8, 6) LGCN_V(8, 12)
+    // one row per group (deep unroll) for the MEAN epilogue, whose reads of E0..E_{K-1} would
+    // otherwise serialise inside a row stream; row bundles (shallow unroll) everywhere else
+    constexpr int U1 = NV >= 8 ? 1 : 8 / NV;
+    constexpr int UB = NV >= 4 ? 1 : 4 / NV;
+    constexpr int RB = G >= 16 ? 15 : G - 1;
+#define LGCN_ARGS rowptr, edges, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, s
+    if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: explicit variants (lgcn_tune)
+#define LGCN_V(R_, U_) \
+        if (g_rows_per_group == R_ && g_unroll == U_) return launch_layer_rpg<V, G, NV, R_, U_>(LGCN_ARGS);
+        LGCN_V(1, 4) LGCN_V(1, 8) LGCN_V(4, 4) LGCN_V(8, 4) LGCN_V(15, 4) LGCN_V(15, 2)
+        LGCN_V(15, 6) LGCN_V(8, 8) LGCN_V(15, 8)
 #undef LGCN_V
     }
-    return launch_layer_rpg<V, G, NV, RPG_MAX, U>(rowptr, edges, n_rows, thr, items, n_items,
-                                                  partials, x, y, ldy, d, dW, ep, s);
+    if (ep.mode == LGCN_EPI_MEAN || RB <= 1 || g_rows_per_group == 1)
+        return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
+    return launch_layer_rpg<V, G, NV, RB, UB>(LGCN_ARGS);
+#undef LGCN_ARGS
 }
 
 template <typename V, int G, int NV>
@@ -657,12 +660,12 @@ int lgcn_tune(int knob, int value) {
     switch (knob) {
         case LGCN_TUNE_ROWS_PER_GROUP: {
             const int old = g_rows_per_group;
-            if (value > 0) g_rows_per_group = value;
+            if (value >= 0) g_rows_per_group = value;
             return old;
         }
         case LGCN_TUNE_UNROLL: {
             const int old = g_unroll;
-            if (value > 0) g_unroll = value;
+            if (value >= 0) g_unroll = value;
             return old;
         }
         default:

@@ -27,8 +27,8 @@ TUNE_ROWS_PER_GROUP, TUNE_UNROLL = 1, 2
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
-DEFAULT_HUB_THRESHOLD = 512
-DEFAULT_HUB_CHUNK = 256
+DEFAULT_HUB_THRESHOLD = 256
+DEFAULT_HUB_CHUNK = int(os.environ.get("LGCN_HUB_CHUNK", "256"))
 
 
 class RowsT(ctypes.Structure):
@@ -182,7 +182,8 @@ class Graph:
             self._rowptr_host = self.rowptr.cpu().numpy()
         return self._rowptr_host
 
-    def hubs(self, threshold, chunk=DEFAULT_HUB_CHUNK):
+    def hubs(self, threshold, chunk=None):
+        chunk = chunk or DEFAULT_HUB_CHUNK
         key = (threshold, chunk)
         if key not in self._plans:
             self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device)

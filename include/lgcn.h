@@ -103,10 +103,10 @@ typedef struct {
 /* ---- identification ---------------------------------------------------------------------- */
 int lgcn_abi_version(void);
 const char* lgcn_error_string(int code);
-/* Tuning knobs (process-global; not needed for correctness — results do not depend on them).
- * Returns the previous value (value <= 0 only queries), or LGCN_EINVAL for an unknown knob. */
-#define LGCN_TUNE_ROWS_PER_GROUP 1  /* rows streamed by one lane group in k_layer (default 8) */
-#define LGCN_TUNE_UNROLL         2  /* gathers in flight per lane group, d = 64 (default 8) */
+/* Tuning knobs (process-global; results never depend on them). 0 = automatic (default).
+ * Returns the previous value (value < 0 only queries), or LGCN_EINVAL for an unknown knob. */
+#define LGCN_TUNE_ROWS_PER_GROUP 1  /* rows streamed by one lane group in k_layer (1 = one row) */
+#define LGCN_TUNE_UNROLL         2  /* gathers in flight per lane group (d = 64 variants) */
 int lgcn_tune(int knob, int value);
 
 /* device properties the host side needs (CU count); returns 0/hipError */

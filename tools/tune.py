@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from gcn_recommendation_amd import engine  # noqa: E402
 
-VARIANTS = [(1, 8), (2, 8), (4, 8), (8, 8), (15, 8), (4, 4), (8, 4), (15, 4), (8, 6), (8, 12)]
+VARIANTS = [(0, 0), (1, 8), (1, 4), (8, 4), (15, 4), (15, 2), (15, 6)]
 
 
 def time_forward(g, segs, K, thr, reps=3):
@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--gens", default="powerlaw,uniform")
     ap.add_argument("--rounds", type=int, default=4)
-    ap.add_argument("--thresholds", default="256,512,2048")
+    ap.add_argument("--thresholds", default="128,256,512")
+    ap.add_argument("--chunks", default="128,256,512")
     args = ap.parse_args()
     lib = engine.load_library()
     dev = torch.device("cuda:0")
@@ -59,22 +60,26 @@ def main():
         thrs = [int(t) for t in args.thresholds.split(",")]
         times = {}
         ref = {}
+        chunks = [int(t) for t in args.chunks.split(",")]
+        combos = [(thr, ch, rpg, u) for thr in thrs for ch in chunks for rpg, u in VARIANTS
+                  if (rpg, u) == (0, 0) or ch == 256]
         for rnd in range(args.rounds):
-            for thr in thrs:
-                for rpg, u in VARIANTS:
+            for thr, ch, rpg, u in combos:
+                    engine.DEFAULT_HUB_CHUNK = ch
+                    g._plans.clear()
                     lib.lgcn_tune(engine.TUNE_ROWS_PER_GROUP, rpg)
                     lib.lgcn_tune(engine.TUNE_UNROLL, u)
                     ms, lay, out = time_forward(g, segs, K, thr)
-                    key = f"thr{thr}_rpg{rpg}_u{u}"
+                    key = f"thr{thr}_ch{ch}_rpg{rpg}_u{u}"
                     times.setdefault(key, []).append((ms, lay))
                     if rnd == 0:
                         h = out[::997].cpu()
-                        if thr not in ref:
-                            ref[thr] = h
-                        elif not torch.equal(ref[thr], h):
+                        if (thr, ch) not in ref:
+                            ref[(thr, ch)] = h
+                        elif not torch.equal(ref[(thr, ch)], h):
                             print(f"!! {gen} {key}: result differs from first variant", flush=True)
-        lib.lgcn_tune(engine.TUNE_ROWS_PER_GROUP, 8)
-        lib.lgcn_tune(engine.TUNE_UNROLL, 8)
+        lib.lgcn_tune(engine.TUNE_ROWS_PER_GROUP, 0)
+        lib.lgcn_tune(engine.TUNE_UNROLL, 0)
         summ = {}
         for k, lst in times.items():
             ms = [x[0] for x in lst]
@@ -84,8 +89,8 @@ def main():
                        "gedges_s": K * nnz / (np.median(ms) / 1e3) / 1e9}
         best = sorted(summ.items(), key=lambda kv: kv[1]["ms_med"])
         for k, s in best:
-            print(f"{gen:9s} {k:22s} {s['ms_med']:8.3f} ms  {s['gedges_s']:6.2f} Gedges/s  "
-                  f"layers {s['layers']}", flush=True)
+            print(f"{gen:9s} {k:28s} {s['ms_med']:8.3f} ms  {s['gedges_s']:6.2f} Gedges/s  "
+                  f"layers {[round(float(x), 3) for x in s['layers']]}", flush=True)
         res[gen] = {"nnz": nnz, "variants": summ}
         del adj, g, segs
         torch.cuda.empty_cache()
