@@ -129,10 +129,13 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
 }
 
 // Rows of one group, RPG at a time: the group walks the bundle's edges as ONE stream (hub rows
-// skipped), keeps U gathers in flight across row boundaries, and folds them in stored order,
-// flushing a row's accumulator (fused epilogue) when the stream passes its end. Each row is still
-// one sequential fmaf chain, so results are identical to RPG = 1; what changes is how many
-// gathers are in flight per group and how many dependent rowptr->edge->gather chains a row pays.
+// skipped) and folds them in stored order, flushing a row's accumulator (fused epilogue) when the
+// stream passes its end. Each row is still one sequential fmaf chain, so results are identical to
+// one row per group; what changes is the latency structure:
+//  * edge records arrive in windows of G records (one coalesced load per window, lane l holding
+//    record wb+l) with the next window prefetched, and reach every lane by shuffles — the only
+//    memory latency left on the critical path is the gather itself;
+//  * U gathers are in flight per group across row boundaries.
 template <typename V, int G, int NV, int MODE, int RPG, int U>
 __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                                             const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
@@ -140,11 +143,15 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                                             float* __restrict__ y, int64_t ldy, int lane, int dW,
                                             const lgcn_epilogue_t& ep) {
     using T = VT<V>;
-    static_assert(RPG < G || G == 64, "row boundaries are held one per lane");
+    static_assert(RPG < G, "row boundaries are held one per lane");
     const int nrows = min(RPG, n_rows - r0);
     // lane l (l <= nrows) holds rowptr[r0 + l]; boundaries are read back by shuffles
     const int32_t rpl = (lane <= nrows) ? rowptr[r0 + lane] : 0;
     auto bnd = [&](int i) { return __shfl(rpl, i, G); };
+    const int32_t eend = bnd(nrows);
+    auto load_win = [&](int32_t b) {
+        return (b + lane < eend) ? load_edge(edges + b + lane) : make_int2(0, 0);
+    };
     V acc[NV];
 #pragma unroll
     for (int q = 0; q < NV; ++q) acc[q] = T::zero();
@@ -153,6 +160,9 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     int32_t lend = bnd(1);
     int32_t j = bnd(0);
     if (lend - j > hub_thr) j = lend;        // hub rows: edges owned by the chunk path
+    int32_t wb = j;                          // window base
+    int2 win = load_win(wb);
+    int2 nxt = load_win(wb + G);
     auto flush = [&](int i) {
         const int32_t deg = bnd(i + 1) - bnd(i);
         if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, r0 + i, lane, dW, acc, y, ldy);
@@ -160,7 +170,8 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
     };
     while (true) {
-        int2 e[U];
+        int col[U];
+        float val[U];
         int rid[U];
         int cnt = 0;
 #pragma unroll
@@ -174,18 +185,30 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                 }
             }
             rid[u] = lr;
+            col[u] = 0;
+            val[u] = 0.f;
             if (lr < nrows) {
-                e[u] = load_edge(edges + j);
+                if (j >= wb + G) {
+                    if (j < wb + 2 * G) {
+                        win = nxt;
+                        wb += G;
+                    } else {  // jumped over a hub row
+                        wb = j;
+                        win = load_win(wb);
+                    }
+                    nxt = load_win(wb + G);
+                }
+                const int idx = j - wb;
+                col[u] = __shfl(win.x, idx, G);
+                val[u] = __int_as_float(__shfl(win.y, idx, G));
                 ++j;
                 ++cnt;
-            } else {
-                e[u] = make_int2(0, 0);
             }
         }
         V xv[U][NV];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float* rp = seg_row(x, e[u].x);
+            const float* rp = seg_row(x, col[u]);
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int c = lane + q * G;
@@ -196,9 +219,8 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
         for (int u = 0; u < U; ++u) {
             if (u < cnt) {
                 while (fr < rid[u]) flush(fr++);
-                const float v = __int_as_float(e[u].y);
 #pragma unroll
-                for (int q = 0; q < NV; ++q) acc[q] = T::fma(v, xv[u][q], acc[q]);
+                for (int q = 0; q < NV; ++q) acc[q] = T::fma(val[u], xv[u][q], acc[q]);
             }
         }
         if (cnt < U) break;
@@ -206,7 +228,25 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     while (fr < nrows) flush(fr++);
 }
 
-template <typename V, int G, int NV, int MODE, int RPG, int U>
+// MEAN epilogue with its NP previous-layer rows loaded before the gathers (they do not depend on
+// them) and pre-summed in the reference order ((E0 + E1) + ...) + E_K.
+template <typename V, int G, int NV, int NP>
+__device__ __forceinline__ void mean_prefetch(const lgcn_epilogue_t& ep, int32_t row, int lane,
+                                              int dW, V (&pre)[NP][NV]) {
+    using T = VT<V>;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const float* src = p == 0 ? seg_row(ep.prev0, row)
+                                  : ep.prev_dense[p - 1] + (int64_t)row * ep.ld_prev;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int c = lane + q * G;
+            pre[p][q] = c < dW ? T::load(src + c * T::W) : T::zero();
+        }
+    }
+}
+
+template <typename V, int G, int NV, int MODE, int RPG, int U, int NP = 0>
 __global__ __launch_bounds__(kBlock) void k_layer(
     const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
     int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
@@ -244,8 +284,24 @@ __global__ __launch_bounds__(kBlock) void k_layer(
         V acc[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
-        accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
-        epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
+        if constexpr (MODE == LGCN_EPI_MEAN && NP > 0) {
+            V pre[NP][NV];
+            mean_prefetch<V, G, NV, NP>(ep, row, lane, dW, pre);
+            accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
+            float* yr = y + (int64_t)row * ldy;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int c = lane + q * G;
+                if (c >= dW) continue;
+                V s = pre[0][q];
+#pragma unroll
+                for (int p = 1; p < NP; ++p) s = T::add(s, pre[p][q]);
+                T::store(yr + c * T::W, T::div(T::add(s, acc[q]), ep.div));
+            }
+        } else {
+            accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
+            epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
+        }
     } else {
         const int64_t r0 = gidx * RPG;
         if (r0 >= n_rows) return;
@@ -447,7 +503,7 @@ bool epi_aligned(const lgcn_epilogue_t& ep) {
 int g_rows_per_group = 0;
 int g_unroll = 0;
 
-template <typename V, int G, int NV, int RPG, int U>
+template <typename V, int G, int NV, int RPG, int U, int NP = 0>
 int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
                      const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                      const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
@@ -466,7 +522,7 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_
                                hub_blocks, partials, x, y, ldy, d, dW, ep);
             break;
         case LGCN_EPI_MEAN:
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN, RPG, U>), dim3((uint32_t)grid),
+            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN, RPG, U, NP>), dim3((uint32_t)grid),
                                dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
                                hub_blocks, partials, x, y, ldy, d, dW, ep);
             break;
@@ -495,12 +551,19 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_ro
     if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: explicit variants (lgcn_tune)
 #define LGCN_V(R_, U_) \
         if (g_rows_per_group == R_ && g_unroll == U_) return launch_layer_rpg<V, G, NV, R_, U_>(LGCN_ARGS);
-        LGCN_V(1, 4) LGCN_V(1, 8) LGCN_V(4, 4) LGCN_V(8, 4) LGCN_V(15, 4) LGCN_V(15, 2)
-        LGCN_V(15, 6) LGCN_V(8, 8) LGCN_V(15, 8)
+        LGCN_V(1, 8) LGCN_V(8, 4) LGCN_V(15, 4) LGCN_V(8, 6) LGCN_V(15, 6) LGCN_V(8, 8)
+        LGCN_V(15, 8)
 #undef LGCN_V
     }
-    if (ep.mode == LGCN_EPI_MEAN || RB <= 1 || g_rows_per_group == 1)
+    if (ep.mode == LGCN_EPI_MEAN) {
+        if (NV <= 2 && g_rows_per_group == 0) {  // early-issued E0..E_{K-1} row loads
+            if (ep.n_prev == 2) return launch_layer_rpg<V, G, NV, 1, U1, 2>(LGCN_ARGS);
+            if (ep.n_prev == 3) return launch_layer_rpg<V, G, NV, 1, U1, 3>(LGCN_ARGS);
+            if (ep.n_prev == 4) return launch_layer_rpg<V, G, NV, 1, U1, 4>(LGCN_ARGS);
+        }
         return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
+    }
+    if (RB <= 1 || g_rows_per_group == 1) return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
     return launch_layer_rpg<V, G, NV, RB, UB>(LGCN_ARGS);
 #undef LGCN_ARGS
 }

@@ -27,7 +27,7 @@ TUNE_ROWS_PER_GROUP, TUNE_UNROLL = 1, 2
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
-DEFAULT_HUB_THRESHOLD = 256
+DEFAULT_HUB_THRESHOLD = 128
 DEFAULT_HUB_CHUNK = int(os.environ.get("LGCN_HUB_CHUNK", "256"))
 
 

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from gcn_recommendation_amd import engine  # noqa: E402
 
-VARIANTS = [(0, 0), (1, 8), (1, 4), (8, 4), (15, 4), (15, 2), (15, 6)]
+VARIANTS = [(0, 0), (1, 8), (8, 4), (15, 4), (8, 6), (15, 6), (8, 8), (15, 8)]
 
 
 def time_forward(g, segs, K, thr, reps=3):
