@@ -1,0 +1,313 @@
+"""Multi-GPU LightGCN propagation on one node: one process per GPU, torch.distributed over RCCL
+(backend "nccl" on ROCm) for the exchange steps, the HIP engine for every local layer.
+
+Two decompositions of E_{k+1} = Â·E_k (models/lightgcn.py:44-46) over P ranks:
+
+rowpart (north_star): Â's rows are cut into P contiguous blocks balanced by nnz + per-row cost;
+    rank p owns rows [R_p, R_{p+1}) with global columns. Layer 1 gathers E0 (replicated
+    parameters) in place; its output slice goes straight into the rank's chunk of a rank-major
+    buffer [P * n_max x d] that one in-place all_gather_into_tensor completes; layers >= 2 read
+    that buffer through column ids remapped to the padded layout once at plan time. The last
+    layer's fused mean reads E0 and the local slices of E1..E_{K-1}; the final slice is
+    all-gathered so every rank holds the full table, as the single-GPU forward returns it.
+    Exchange per layer: (P-1)/P * N * d * 4 bytes per rank.
+
+featsplit: every rank holds the whole CSR (0.45 GB at Books scale) and d/P embedding columns
+    (column-parallel embedding tables); columns of an SpMM are independent, so the K layers
+    need NO exchange. The output stays column-sharded; consumers reduce partial dot products
+    (bpr_loss_featsplit: one all_reduce of B floats per loss).
+
+On a CPU tensor the local layer is the reference's ATen op (used by the gloo tests of the
+orchestration); a HIP tensor always runs the engine.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import engine
+
+
+# ----------------------------------------------------------------------------------------------
+# process group
+# ----------------------------------------------------------------------------------------------
+def init(device_type="cuda"):
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    backend = "nccl" if device_type == "cuda" else "gloo"
+    kw = {}
+    if device_type == "cuda":
+        kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend, **kw)
+    return dist.get_rank(), dist.get_world_size()
+
+
+def shutdown():
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------
+# row partition planning (host)
+# ----------------------------------------------------------------------------------------------
+def balanced_row_bounds(deg, world, row_cost=4.0):
+    """Contiguous row blocks with near-equal (nnz + row_cost * rows): P+1 boundaries."""
+    deg = np.asarray(deg, dtype=np.float64)
+    n = deg.size
+    cum = np.concatenate([[0.0], np.cumsum(deg + row_cost)])
+    targets = cum[-1] * np.arange(world + 1) / world
+    b = np.searchsorted(cum, targets, side="left").astype(np.int64)
+    b[0], b[-1] = 0, n
+    return np.maximum.accumulate(np.minimum(b, n))
+
+
+def layout_positions(bounds, n_max, ids):
+    """Global row id -> position in the rank-major padded buffer [P * n_max]."""
+    ids = np.asarray(ids, dtype=np.int64)
+    owner = np.searchsorted(bounds, ids, side="right") - 1
+    return owner * n_max + (ids - bounds[owner])
+
+
+def feature_bounds(d, world):
+    """Column blocks per rank, multiples of 4 floats where d allows (16-B aligned gathers)."""
+    unit = 4 if d % 4 == 0 and d // 4 >= world else 1
+    units = d // unit
+    cuts = [(units * p) // world * unit for p in range(world + 1)]
+    cuts[-1] = d
+    return np.asarray(cuts, dtype=np.int64)
+
+
+class RowPartPlan:
+    """Rank-local row block of a row-sorted global COO (r, c, v) with n nodes."""
+
+    def __init__(self, r, c, v, n, world, rank, device, row_cost=4.0):
+        rowptr_g = np.searchsorted(r, np.arange(n + 1)).astype(np.int64)
+        self.bounds = balanced_row_bounds(np.diff(rowptr_g), world, row_cost)
+        self.n, self.world, self.rank, self.device = n, world, rank, device
+        self.n_max = int(np.diff(self.bounds).max())
+        self.r0, self.r1 = int(self.bounds[rank]), int(self.bounds[rank + 1])
+        self.n_local = self.r1 - self.r0
+        e0, e1 = rowptr_g[self.r0], rowptr_g[self.r1]
+        self.rowptr = (rowptr_g[self.r0:self.r1 + 1] - e0).astype(np.int32)
+        self.cols = np.asarray(c[e0:e1], dtype=np.int64)
+        self.cols_layout = layout_positions(self.bounds, self.n_max, self.cols)
+        self.vals = np.asarray(v[e0:e1], dtype=np.float32)
+        self.nnz_local = int(e1 - e0)
+        if torch.device(device).type == "cuda":
+            self.g1 = engine.graph_from_host_csr(self.rowptr, self.cols, self.vals, n, device)
+            self.gk = engine.graph_from_host_csr(self.rowptr, self.cols_layout, self.vals,
+                                                 world * self.n_max, device)
+        else:
+            self.g1 = self._cpu_coo(self.cols, n)
+            self.gk = self._cpu_coo(self.cols_layout, world * self.n_max)
+
+    def _cpu_coo(self, cols, n_cols):
+        rows = np.repeat(np.arange(self.n_local), np.diff(self.rowptr))
+        idx = torch.from_numpy(np.vstack([rows, cols]))
+        return torch.sparse_coo_tensor(idx, torch.from_numpy(self.vals), (self.n_local, n_cols))
+
+    def exchange_bytes_per_layer(self, d):
+        return (self.world - 1) * self.n_max * d * 4
+
+
+def _local_layer(graph, xs, y, d, ep, hub_thr):
+    """y[:n_local] = epilogue(Â_local · X): engine on HIP, the reference ATen op on CPU."""
+    if y.device.type == "cuda":
+        return engine.spmm_layer(graph, xs, y, d, ep, hub_thr)
+    x = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
+    y.copy_(torch.sparse.mm(graph, x))
+    return y
+
+
+def rowpart_buffers(plan, K, d, dev):
+    """Layer buffers in the rank-major padded layout + this rank's (padded) final rows."""
+    bufs = [torch.empty((plan.world * plan.n_max, d), dtype=torch.float32, device=dev)
+            for _ in range(K - 1)]
+    return bufs, torch.empty((plan.n_max, d), dtype=torch.float32, device=dev)
+
+
+def rowpart_layer(plan, k, K, segments, bufs, out_local, hub_thr):
+    """Local part of layer k (1-based): writes this rank's slice of E_k into bufs[k-1], or, for
+    k == K, the fused mean of its rows into out_local[:n_local]."""
+    d = segments[0].shape[1]
+    on_gpu = segments[0].device.type == "cuda"
+    rk, nm, nl = plan.rank, plan.n_max, plan.n_local
+    g = plan.g1 if k == 1 else plan.gk
+    xs = segments if k == 1 else [bufs[k - 2]]
+    if k < K:
+        mine = bufs[k - 1][rk * nm: rk * nm + nl]
+        _local_layer(g, xs, mine, d, engine._epilogue(engine.LGCN_EPI_STORE) if on_gpu else None,
+                     hub_thr)
+        return
+    prev = [b[rk * nm: rk * nm + nl] for b in bufs]
+    if on_gpu:
+        ep = engine._epilogue(engine.LGCN_EPI_MEAN, prev0=engine.rows_desc_from(segments, plan.r0, d),
+                              prev_dense=prev, ld_prev=d, div=float(K + 1))
+        _local_layer(g, xs, out_local[:nl], d, ep, hub_thr)
+    else:  # reference order ((E0 + E1) + ...) + E_K, then / (K+1)
+        last = torch.empty((nl, d), dtype=torch.float32)
+        _local_layer(g, xs, last, d, None, hub_thr)
+        s_ = torch.cat(segments, 0)[plan.r0:plan.r1].clone()
+        for p_ in prev:
+            s_ = s_ + p_
+        out_local[:nl].copy_((s_ + last) / (K + 1))
+
+
+def rowpart_forward(plan, segments, K, hub_thr=None, gather_final=True, layer_events=None):
+    """K-layer propagation + mean over a row partition. segments: replicated E0 blocks
+    (user, item[, brand]) in global row order. Returns the final table in layout order
+    [P * n_max x d] (gather_final) or the local final rows [n_local x d]."""
+    if hub_thr is None:
+        hub_thr = engine.hub_threshold_from_env()
+    d = segments[0].shape[1]
+    dev = segments[0].device
+    W, rk, nm, nl = plan.world, plan.rank, plan.n_max, plan.n_local
+    bufs, out_local = rowpart_buffers(plan, K, d, dev)
+    if K == 0:
+        out_local[:nl].copy_(torch.cat(segments, 0)[plan.r0:plan.r1])
+    for k in range(1, K + 1):
+        if layer_events is not None:
+            layer_events[k - 1][0].record()
+        rowpart_layer(plan, k, K, segments, bufs, out_local, hub_thr)
+        if layer_events is not None:
+            layer_events[k - 1][1].record()
+        if k < K:  # in-place all-gather: this rank's chunk is already in place
+            dist.all_gather_into_tensor(bufs[k - 1], bufs[k - 1][rk * nm:(rk + 1) * nm])
+    if not gather_final:
+        return out_local[:nl]
+    full = torch.empty((W * nm, d), dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(full, out_local)
+    return full
+
+
+def layout_to_global(plan, table):
+    """Rows of a layout-ordered table [P * n_max x d] back in global order [n x d] (a copy)."""
+    parts = [table[p * plan.n_max: p * plan.n_max + int(plan.bounds[p + 1] - plan.bounds[p])]
+             for p in range(plan.world)]
+    return torch.cat(parts, 0)
+
+
+# ----------------------------------------------------------------------------------------------
+# feature split
+# ----------------------------------------------------------------------------------------------
+def featsplit_slices(segments, world, rank):
+    """This rank's column block of every E0 segment (contiguous copies: the parameter shard)."""
+    d = segments[0].shape[1]
+    cb = feature_bounds(d, world)
+    c0, c1 = int(cb[rank]), int(cb[rank + 1])
+    return [t[:, c0:c1].contiguous() for t in segments], (c0, c1)
+
+
+def featsplit_forward(graph, seg_slices, K, hub_thr=None, layer_events=None):
+    """K layers + mean on this rank's columns: no exchange at all."""
+    if seg_slices[0].device.type == "cuda":
+        return engine.propagate_forward(graph, seg_slices, K, hub_thr, layer_events=layer_events)
+    ego = torch.cat(seg_slices, 0)
+    all_e, x = [ego], ego
+    for _ in range(K):
+        x = torch.sparse.mm(graph, x)
+        all_e.append(x)
+    return torch.mean(torch.stack(all_e, 0), 0)
+
+
+def bpr_loss_featsplit(u_slice, p_slice, n_slice, u0_slice, p0_slice, n0_slice, lambda_reg):
+    """bpr_loss_reg (main.py:366-402) on column-sharded rows: partial dot products and partial
+    squared norms are summed over ranks with ONE all_reduce of 2B+1 floats."""
+    B = u_slice.shape[0]
+    part = torch.cat([(u_slice * p_slice).sum(1), (u_slice * n_slice).sum(1),
+                      (u0_slice.pow(2).sum() + p0_slice.pow(2).sum() +
+                       n0_slice.pow(2).sum()).reshape(1)])
+    dist.all_reduce(part)
+    pos, neg, sq = part[:B], part[B:2 * B], part[2 * B]
+    bpr = -torch.mean(torch.log(torch.sigmoid(pos - neg) + 1e-8))
+    return bpr + lambda_reg * sq / float(B)
+
+
+# ----------------------------------------------------------------------------------------------
+# bench driver (bench.py, N > 1)
+# ----------------------------------------------------------------------------------------------
+def _timed(fn, steps, warmup, dev):
+    for _ in range(warmup):
+        fn(None)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    evs = []
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(steps):
+        ev = fn(True)
+        evs.append(ev)
+    t1.record()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    ms = t0.elapsed_time(t1)
+    lay = np.array([[a.elapsed_time(b) for a, b in e] for e in evs])
+    return ms, lay
+
+
+def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
+    rank, world = init("cuda")
+    d, K = cfg["d"], cfg["K"]
+    U, I = cfg["users"], cfg["items"]
+    n = U + I
+    nnz = len(v)
+    mode = args.mode
+
+    def mk_events():
+        return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(K)]
+
+    if mode == "featsplit":
+        rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
+        g = engine.graph_from_host_csr(rowptr, c, v, n, dev)
+        slices, (c0, c1) = featsplit_slices(emb_host, world, rank)
+        slices = [t.to(dev) for t in slices]
+        dl = c1 - c0
+        g.hubs(hub_thr)
+
+        def fn(timed):
+            ev = mk_events() if timed else None
+            featsplit_forward(g, slices, K, hub_thr, layer_events=ev)
+            return ev
+        b_layer = nnz * (4 * dl + 8) + 4 * (n + 1) + 4 * n * dl
+        comm = 0
+        extra = {"columns": [int(c0), int(c1)]}
+    else:
+        plan = RowPartPlan(r, c, v, n, world, rank, dev)
+        segs = [t.to(dev) for t in emb_host]
+
+        def fn(timed):
+            ev = mk_events() if timed else None
+            rowpart_forward(plan, segs, K, hub_thr, gather_final=True, layer_events=ev)
+            return ev
+        b_layer = plan.nnz_local * (4 * d + 8) + 4 * (plan.n_local + 1) + 4 * plan.n_local * d
+        comm = K * plan.exchange_bytes_per_layer(d)
+        extra = {"rows": [plan.r0, plan.r1], "nnz_local": plan.nnz_local}
+
+    ms, lay = _timed(fn, args.steps, args.warmup, dev)
+    t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
+                     dtype=torch.float64, device=dev)
+    tmax = t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    ms_max, kern_ms, all_ms = (float(x) for x in tmax.tolist())
+    value = K * nnz * args.steps / (ms_max / 1e3)
+    achieved = b_layer / (kern_ms / 1e3) / 1e9
+    return {
+        "metric": "propagated edges/sec (SpMM) + Recall@20, Amazon-Books 3-layer d=64",
+        "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_max / args.steps, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": cfg["name"], "generator": args.gen, "users": U, "items": I,
+                   "interactions": cfg["interactions"], "nnz": nnz, "d": d, "layers": K,
+                   "hub_threshold": hub_thr, "parallelism": f"{mode}{world}",
+                   "exchange_bytes_per_step_per_rank": int(comm), **extra},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
+                     "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "kernel": "k_layer store layers, per GPU (max over ranks)",
+                     "bytes_per_launch": int(b_layer), "avg_launch_ms": round(kern_ms, 4)},
+    }

@@ -125,6 +125,40 @@ def rows_desc(segments, ld):
     return RowsT(ps[0], ps[1], ps[2], ends[0], ends[1], ld)
 
 
+def rows_desc_from(segments, start, ld):
+    """lgcn_rows_t whose row 0 is global row `start` of the concatenation of `segments`
+    (a rank's local rows reading E0 in place: segment bases shifted, ends rebased)."""
+    ps, ends, acc = [], [], 0
+    for t in segments:
+        ps.append(t.data_ptr() + (acc - start) * ld * t.element_size())
+        acc += t.shape[0]
+        ends.append(max(acc - start, 0))
+    while len(ps) < 3:
+        ps.append(ps[-1])
+        ends.append(ends[-1])
+    return RowsT(ps[0], ps[1], ps[2], ends[0], ends[1], ld)
+
+
+def pack_edges(cols, vals):
+    """Host {int32 col, fp32 val} edge records (lgcn_edge_t) from numpy arrays."""
+    c = np.asarray(cols, dtype=np.int64).astype(np.uint32).astype(np.uint64)
+    v = np.asarray(vals, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return ((v << np.uint64(32)) | c).view(np.int64)
+
+
+def graph_from_host_csr(rowptr, cols, vals, n_cols, device):
+    """Device CSR (possibly rectangular: a rank's row block with global columns) from host
+    arrays already in the engine's order. Forward-only: no transpose is attached."""
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int32)
+    n_rows = rowptr.size - 1
+    nnz = int(rowptr[-1])
+    edges = pack_edges(cols, vals) if nnz else np.zeros(1, np.int64)
+    g = Graph(n_rows, n_cols, torch.from_numpy(rowptr).to(device),
+              torch.from_numpy(edges).to(device), nnz, device)
+    g._rowptr_host = rowptr
+    return g
+
+
 def hub_threshold_from_env(default=DEFAULT_HUB_THRESHOLD):
     v = os.environ.get("LGCN_HUB_THRESHOLD", "")
     if v.lower() in ("exact", "inf", "none", "off"):
