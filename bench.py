@@ -210,10 +210,16 @@ def main():
             "hub_rows": int(hub_rows.size), "max_degree": int(g.degrees().max())}
         del f64
         rp = np.searchsorted(r, np.arange(n + 1)).astype(np.int64)
-        rg = recall_ndcg(out[:U], out[U:], ev_users, ev_items, rp, c, U, k=20)
-        rc = recall_ndcg(ref[:U].to(dev), ref[U:].to(dev), ev_users, ev_items, rp, c, U, k=20)
+        rg = recall_ndcg(out[:U], out[U:], ev_users, ev_items, rp, c, U, k=20, return_topk=True)
+        rc = recall_ndcg(ref[:U].to(dev), ref[U:].to(dev), ev_users, ev_items, rp, c, U, k=20,
+                         return_topk=True)
         result["recall20"] = {"gpu": rg[0], "cpu": rc[0], "ndcg_gpu": rg[1], "ndcg_cpu": rc[1],
-                              "identical": rg == rc, "users": int(len(ev_users))}
+                              "identical": rg[:2] == rc[:2], "users": int(len(ev_users)),
+                              "top20_lists_identical_frac": float(
+                                  np.all(rg[2] == rc[2], axis=1).mean()),
+                              "note": "random-init embeddings and random held-out items: recall "
+                                      "is ~0 by construction; the top-20 list agreement is the "
+                                      "informative parity number"}
     print(json.dumps(result), flush=True)
 
 

@@ -130,7 +130,9 @@ def rows_desc_from(segments, start, ld):
     (a rank's local rows reading E0 in place: segment bases shifted, ends rebased)."""
     ps, ends, acc = [], [], 0
     for t in segments:
-        ps.append(t.data_ptr() + (acc - start) * ld * t.element_size())
+        # the kernel addresses local row i of segment s as p_s + (i - end_{s-1}) * ld, and
+        # local row end_{s-1} is this segment's row max(start - acc, 0)
+        ps.append(t.data_ptr() + max(start - acc, 0) * ld * t.element_size())
         acc += t.shape[0]
         ends.append(max(acc - start, 0))
     while len(ps) < 3:

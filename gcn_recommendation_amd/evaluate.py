@@ -10,13 +10,13 @@ import torch
 
 
 def recall_ndcg(user_emb, item_emb, users, heldout_items, train_rowptr, train_cols, U, k=20,
-                batch_size=1024):
+                batch_size=1024, return_topk=False):
     """users: int64 [n] user ids; heldout_items: int64 [n] item ids (one per user);
     train_rowptr/train_cols: host CSR of Â (numpy) — a user row's cols >= U are its items."""
     dev = user_emb.device
     users = np.asarray(users, dtype=np.int64)
     heldout_items = np.asarray(heldout_items, dtype=np.int64)
-    hits, ndcgs = [], []
+    hits, ndcgs, tops = [], [], []
     with torch.no_grad():
         for s in range(0, len(users), batch_size):
             bu = users[s:s + batch_size]
@@ -31,9 +31,13 @@ def recall_ndcg(user_emb, item_emb, users, heldout_items, train_rowptr, train_co
                        torch.from_numpy(cc[keep] - U).to(dev)] = -1e10
             _, top = torch.topk(scores, k=k)
             top = top.cpu().numpy()
+            if return_topk:
+                tops.append(top)
             truth = heldout_items[s:s + batch_size]
             for j in range(len(bu)):
                 pos = np.nonzero(top[j] == truth[j])[0]
                 hits.append(1 if pos.size else 0)
                 ndcgs.append(1 / np.log2(pos[0] + 2) if pos.size else 0)
+    if return_topk:
+        return float(np.mean(hits)), float(np.mean(ndcgs)), np.concatenate(tops)
     return float(np.mean(hits)), float(np.mean(ndcgs))

@@ -34,3 +34,26 @@ def test_env_threshold(monkeypatch):
     assert engine.hub_threshold_from_env() == 64
     monkeypatch.delenv("LGCN_HUB_THRESHOLD")
     assert engine.hub_threshold_from_env() == engine.DEFAULT_HUB_THRESHOLD
+
+
+def test_rows_desc_from_addresses_global_rows():
+    """Host check of the segment descriptor a rank uses to read E0 rows in place: local row i
+    must address global row start+i of cat(segments) (a GPU fault in round 1 came from a
+    sign error here)."""
+    import torch
+    d = 8
+    segs = [torch.zeros(5, d), torch.zeros(7, d), torch.zeros(3, d)]
+    glob = [(t, r) for t in segs for r in range(t.shape[0])]
+    for start in (0, 2, 5, 6, 12, 14):
+        desc = engine.rows_desc_from(segs, start, d)
+        ptrs, ends = [desc.p0, desc.p1, desc.p2], [desc.end0, desc.end1]
+        for i in range(15 - start):
+            s = 0 if i < ends[0] else (1 if i < ends[1] else 2)
+            if s == 0:
+                addr = ptrs[0] + i * d * 4
+            elif s == 1:
+                addr = ptrs[1] + (i - ends[0]) * d * 4
+            else:
+                addr = ptrs[2] + (i - ends[1]) * d * 4
+            t, r = glob[start + i]
+            assert addr == t.data_ptr() + r * d * 4, (start, i)

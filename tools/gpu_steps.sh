@@ -13,4 +13,8 @@ for spec in "$@"; do
   echo "=== $name rc=$rc ($(( $(date +%s) - start ))s)"
   tail -n 8 "gpurun_out/$name.log"
   case $rc in 0|1|2|5) ;; *) echo "=== fatal rc=$rc: stopping"; exit "$rc";; esac
+  # a GPU fault caught as a Python exception still ends the call
+  if grep -q -E "illegal memory access|hipErrorIllegalAddress|Memory access fault|HSA_STATUS_ERROR|page fault" "gpurun_out/$name.log"; then
+    echo "=== GPU fault signature in $name.log: stopping"; exit 99
+  fi
 done
