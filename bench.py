@@ -67,6 +67,62 @@ def xavier(rows, d, gen):
     return (torch.rand(rows, d, generator=gen) * 2 - 1) * bound
 
 
+def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
+    """main.py's per-batch hot loop (main.py:488-531) with the drop-in model: full-graph forward
+    through the engine, batch gathers, bpr_loss_reg, backward (K engine layers), Adam step.
+    Edges/s counts the 2K propagated layers (K forward + K backward)."""
+    from gcn_recommendation_amd.loss import bpr_loss_reg
+    from models.lightgcn import LightGCN
+
+    class Cfg:
+        embedding_dim, n_layers, debug = d, K, False
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = LightGCN.__new__(LightGCN)
+        torch.nn.Module.__init__(model)
+        model.num_users, model.num_items, model.num_brands = U, I, 0
+        model.embedding_dim, model.n_layers, model.debug = d, K, False
+        model.user_embedding = torch.nn.Embedding.from_pretrained(emb_host[0].clone(), freeze=False)
+        model.brand_embedding = torch.nn.Embedding(0, d)
+        model.item_embedding = torch.nn.Embedding.from_pretrained(emb_host[1].clone(), freeze=False)
+        model.final_brand_emb, model._graph_adj = None, None
+    model = model.to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    rng = np.random.default_rng(0)
+    batches = [tuple(torch.from_numpy(x).to(dev) for x in (rng.integers(0, U, 2048),
+                                                            rng.integers(0, I, 2048),
+                                                            rng.integers(0, I, 2048)))
+               for _ in range(args.train_steps + 2)]
+
+    def step(b):
+        users, pos, neg = b
+        opt.zero_grad()
+        fu, fi, fb, u0, i0 = model(adj, use_brand=False)
+        loss = bpr_loss_reg(fu[users], fi[pos], fi[neg], u0[users], i0[pos], i0[neg], 1e-4)
+        loss.backward()
+        opt.step()
+        return loss
+    for b in batches[:2]:
+        step(b)
+    torch.cuda.synchronize()
+    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for b in batches[2:]:
+        loss = step(b)
+    e.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(e) / args.train_steps
+    nnz = adj._nnz()
+    out = {"ms_per_step": round(ms, 3), "propagated_edges_per_s": round(2 * K * nnz / (ms / 1e3), 1),
+           "batch": 2048, "optimizer": "Adam(lr=1e-3)", "loss_last": float(loss.item()),
+           "what": "main.py:488-531 hot loop: forward + gathers + bpr_loss_reg + backward + "
+                   "Adam over all 14.7M x 64 parameters"}
+    del model, opt
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +133,8 @@ def main():
     ap.add_argument("--hub-threshold", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--recall-users", type=int, default=2048)
+    ap.add_argument("--train-steps", type=int, default=5,
+                    help="also time main.py's training step (forward+BPR+backward+Adam)")
     ap.add_argument("--mode", default="featsplit", choices=["rowpart", "featsplit"],
                     help="multi-GPU decomposition (N>1)")
     ap.add_argument("--force-dist", action="store_true",
@@ -176,6 +234,9 @@ def main():
         "roofline": roof,
         "wall_s_timed": round(wall, 3), "prep_s": round(prep_s, 2),
     }
+
+    if args.train_steps > 0:
+        result["train_step"] = bench_train_step(adj, emb_host, U, I, d, K, dev, args)
 
     # parity + Recall@20 vs the reference CPU path (torch.sparse.mm restated in oracle/)
     if not args.no_cpu_baseline:
