@@ -35,6 +35,14 @@ CONFIGS = {
     # BASELINE.json configs[1]: Books subset
     "c2": dict(users=50_000, items=50_000, interactions=1_000_000, d=64, K=3, seed=2,
                name="C2 Amazon-Books subset shape (50k x 50k x 1M interactions)"),
+    # BASELINE.json configs[3]: full Books, d=256, 4 layers (8-GPU config; runs on 1 GPU too)
+    "c4": dict(users=10_300_000, items=4_400_000, interactions=29_500_000, d=256, K=4, seed=3,
+               name="C4 full Amazon-Books-2023 shape, d=256, 4 layers"),
+    # BASELINE.json configs[4]: Fusion path: Books + brand nodes (I/10, one per item) + content
+    # embeddings C=64, d=128 (the LightGCN_Fusion forward: Linear+leaky_relu, then propagation)
+    "c5": dict(users=10_300_000, items=4_400_000, interactions=29_500_000, d=128, K=3, seed=3,
+               brands=440_000, content=64,
+               name="C5 LightGCN_Fusion, Books shape + 440k brands, content C=64, d=128"),
 }
 
 
@@ -50,15 +58,21 @@ def make_graph(cfg, gen, heldout_users):
         u, i = graph.uniform_interactions(U, I, E, cfg["seed"])
     else:
         u, i = graph.powerlaw_interactions(U, I, E, cfg["seed"])
-    rows, cols = graph.edge_lists(u, i, U, I, use_brand=False)
+    B = cfg.get("brands", 0)
+    if B:
+        ib_item = np.arange(I)
+        ib_brand = np.random.default_rng(cfg["seed"] + 7).integers(0, B, I)
+        rows, cols = graph.edge_lists(u, i, U, I, ib_item, ib_brand, use_brand=True)
+    else:
+        rows, cols = graph.edge_lists(u, i, U, I, use_brand=False)
     del u, i
-    r, c, v = graph.normalise(rows, cols, U + I)
+    r, c, v = graph.normalise(rows, cols, U + I + B)
     del rows, cols
     # held-out items for Recall@20 parity: one random item per sampled user (not in Â)
     rng = np.random.default_rng(cfg["seed"] + 100)
     ev_users = rng.choice(U, size=min(heldout_users, U), replace=False)
     ev_items = rng.integers(0, I, ev_users.size)
-    log(f"[bench] graph {gen}: N={U + I:,} nnz={len(v):,} built in {time.time() - t0:.1f}s")
+    log(f"[bench] graph {gen}: N={U + I + B:,} nnz={len(v):,} built in {time.time() - t0:.1f}s")
     return r, c, v, ev_users, ev_items
 
 
@@ -154,11 +168,12 @@ def main():
     hub_thr = args.hub_threshold if args.hub_threshold is not None else engine.hub_threshold_from_env()
 
     r, c, v, ev_users, ev_items = make_graph(cfg, args.gen, args.recall_users)
-    U, I = cfg["users"], cfg["items"]
-    n = U + I
+    U, I, B = cfg["users"], cfg["items"], cfg.get("brands", 0)
+    n = U + I + B
     nnz = len(v)
     gen = torch.Generator().manual_seed(42)
-    emb_host = [xavier(U, d, gen), xavier(I, d, gen)]
+    emb_host = [xavier(U, d, gen), xavier(I, d, gen)] + ([xavier(B, d, gen)] if B else [])
+    fusion = cfg.get("content", 0)
 
     if world > 1 or args.force_dist:
         from gcn_recommendation_amd import dist
@@ -181,8 +196,22 @@ def main():
     log(f"[bench] CSR plan {prep_s:.2f}s; hubs: {hp.n_rows} rows / {hp.n_items} chunks "
         f"(threshold {hub_thr}); max degree {int(g.degrees().max())}")
 
+    if fusion:  # LightGCN_Fusion forward: [user | leaky_relu(Linear([id | content])) | brand]
+        content = torch.from_numpy(np.random.default_rng(5).standard_normal(
+            (I, fusion)).astype(np.float32)).to(dev)
+        lin = torch.nn.Linear(d + fusion, d).to(dev)
+
+        def step(ev=None):
+            with torch.no_grad():
+                fused = torch.nn.functional.leaky_relu(lin(torch.cat([segs[1], content], 1)))
+                return engine.propagate_forward(g, [segs[0], fused] + segs[2:], K, hub_thr,
+                                                layer_events=ev)
+    else:
+        def step(ev=None):
+            return engine.propagate_forward(g, segs, K, hub_thr, layer_events=ev)
+
     for _ in range(args.warmup):
-        engine.propagate_forward(g, segs, K, hub_thr)
+        step()
     torch.cuda.synchronize()
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for _ in range(K)] for _ in range(args.steps)]
@@ -191,7 +220,7 @@ def main():
     t_wall = time.time()
     start.record()
     for s in range(args.steps):
-        out = engine.propagate_forward(g, segs, K, hub_thr, layer_events=evs[s])
+        out = step(evs[s])
     stop.record()
     torch.cuda.synchronize()
     wall = time.time() - t_wall
@@ -230,16 +259,17 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": cfg["name"], "generator": args.gen, "users": U, "items": I,
                    "interactions": cfg["interactions"], "nnz": nnz, "d": d, "layers": K,
+                   "brands": B, "content_dim": fusion,
                    "hub_threshold": hub_thr, "parallelism": "single"},
         "roofline": roof,
         "wall_s_timed": round(wall, 3), "prep_s": round(prep_s, 2),
     }
 
-    if args.train_steps > 0:
+    if args.train_steps > 0 and not fusion and not B:
         result["train_step"] = bench_train_step(adj, emb_host, U, I, d, K, dev, args)
 
     # parity + Recall@20 vs the reference CPU path (torch.sparse.mm restated in oracle/)
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and not fusion and d * (K + 1) <= 256:
         from oracle import oracle
         adj_cpu = torch.sparse_coo_tensor(torch.from_numpy(np.vstack((r, c))), torch.from_numpy(v),
                                           (n, n))

@@ -42,6 +42,7 @@ def test_training_loop_gpu_matches_cpu(gpu_device):
     lg, pg = _train(gpu_device, z)
     lc, pc = _train(torch.device("cpu"), z)
     np.testing.assert_allclose(lg, lc, rtol=1e-5)
+    z0 = {k[len("param/"):]: z[k] for k in z.files if k.startswith("param/")}
     for k in pc:
         np.testing.assert_allclose(pg[k], pc[k], rtol=0, atol=2e-6 * np.abs(pc[k]).max() + 1e-9)
-    assert lg[-1] < lg[0]
+        assert not np.array_equal(pc[k], z0[k]) or pc[k].size == 0, f"{k} never updated"
