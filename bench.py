@@ -51,7 +51,7 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def make_graph(cfg, gen, heldout_users):
+def make_graph(cfg, gen, heldout_users, keep_interactions=False):
     t0 = time.time()
     U, I, E = cfg["users"], cfg["items"], cfg["interactions"]
     if gen == "uniform":
@@ -59,21 +59,20 @@ def make_graph(cfg, gen, heldout_users):
     else:
         u, i = graph.powerlaw_interactions(U, I, E, cfg["seed"])
     B = cfg.get("brands", 0)
-    if B:
-        ib_item = np.arange(I)
-        ib_brand = np.random.default_rng(cfg["seed"] + 7).integers(0, B, I)
-        rows, cols = graph.edge_lists(u, i, U, I, ib_item, ib_brand, use_brand=True)
-    else:
-        rows, cols = graph.edge_lists(u, i, U, I, use_brand=False)
-    del u, i
+    ib = (np.arange(I), np.random.default_rng(cfg["seed"] + 7).integers(0, B, I)) if B else (None, None)
+    t1 = time.time()
+    rows, cols = graph.edge_lists(u, i, U, I, ib[0], ib[1], use_brand=bool(B))
     r, c, v = graph.normalise(rows, cols, U + I + B)
     del rows, cols
+    t_norm = time.time() - t1
     # held-out items for Recall@20 parity: one random item per sampled user (not in Â)
     rng = np.random.default_rng(cfg["seed"] + 100)
     ev_users = rng.choice(U, size=min(heldout_users, U), replace=False)
     ev_items = rng.integers(0, I, ev_users.size)
-    log(f"[bench] graph {gen}: N={U + I + B:,} nnz={len(v):,} built in {time.time() - t0:.1f}s")
-    return r, c, v, ev_users, ev_items
+    log(f"[bench] graph {gen}: N={U + I + B:,} nnz={len(v):,} built in {time.time() - t0:.1f}s "
+        f"(host normalise {t_norm:.1f}s)")
+    inter = (u, i, ib, t_norm) if keep_interactions else None
+    return r, c, v, ev_users, ev_items, inter
 
 
 def xavier(rows, d, gen):
@@ -167,7 +166,8 @@ def main():
     engine.load_library()
     hub_thr = args.hub_threshold if args.hub_threshold is not None else engine.hub_threshold_from_env()
 
-    r, c, v, ev_users, ev_items = make_graph(cfg, args.gen, args.recall_users)
+    r, c, v, ev_users, ev_items, inter = make_graph(cfg, args.gen, args.recall_users,
+                                                    keep_interactions=(world == 1))
     U, I, B = cfg["users"], cfg["items"], cfg.get("brands", 0)
     n = U + I + B
     nnz = len(v)
@@ -193,6 +193,17 @@ def main():
     torch.cuda.synchronize()
     prep_s = time.time() - t0
     segs = [t.to(dev) for t in emb_host]
+    # the device adjacency builder on the same interactions: time + bitwise
+    u_, i_, ib_, t_norm = inter
+    torch.cuda.synchronize()
+    t0 = time.time()
+    adj_dev = graph.build_norm_adj_device(u_, i_, U, I, B, ib_[0], ib_[1], bool(B), device=dev)
+    torch.cuda.synchronize()
+    t_dev = time.time() - t0
+    builder = {"host_numpy_s": round(t_norm, 2), "device_s": round(t_dev, 2),
+               "bitwise_equal": bool(torch.equal(adj_dev._indices(), adj._indices()) and torch.equal(
+                   adj_dev._values().view(torch.int32), adj._values().view(torch.int32)))}
+    del adj_dev, inter, u_, i_
     log(f"[bench] CSR plan {prep_s:.2f}s; hubs: {hp.n_rows} rows / {hp.n_items} chunks "
         f"(threshold {hub_thr}); max degree {int(g.degrees().max())}")
 
@@ -263,6 +274,7 @@ def main():
                    "hub_threshold": hub_thr, "parallelism": "single"},
         "roofline": roof,
         "wall_s_timed": round(wall, 3), "prep_s": round(prep_s, 2),
+        "adjacency_build": builder,
     }
 
     if args.train_steps > 0 and not fusion and not B:

@@ -450,6 +450,39 @@ __global__ void k_csr_symmetric(const int32_t* __restrict__ rowptr,
 }
 
 // ---------------------------------------------------------------------------------------------
+// adjacency builder (main.py:313-336 on the device): degree histogram, duplicate merge by a
+// 64-bit radix sort of row*n+col keys + run-length encode, values fp32((d_r * m) * d_c)
+// ---------------------------------------------------------------------------------------------
+__global__ void k_adj_degree(const int64_t* __restrict__ rows, int64_t n_edges,
+                             int32_t* __restrict__ deg) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_edges) atomicAdd(deg + rows[j], 1);  // integer adds: order-independent
+}
+
+__global__ void k_adj_keys(const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
+                           int64_t n_edges, int64_t n, uint64_t* __restrict__ keys) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_edges) keys[j] = (uint64_t)rows[j] * (uint64_t)n + (uint64_t)cols[j];
+}
+
+__global__ void k_adj_finish(const uint64_t* __restrict__ uniq, const int32_t* __restrict__ counts,
+                             int64_t nnz, int64_t n, const float* __restrict__ dinv,
+                             int64_t* __restrict__ coo_rows, int64_t* __restrict__ coo_cols,
+                             float* __restrict__ vals, lgcn_edge_t* __restrict__ edges) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    const uint64_t k = uniq[j];
+    const int64_t r = (int64_t)(k / (uint64_t)n);
+    const int64_t c = (int64_t)(k - (uint64_t)r * (uint64_t)n);
+    // scipy: D.dot(A) -> d_r * m ; .dot(D) -> (d_r * m) * d_c   (fp32, each product rounded)
+    const float v = __fmul_rn(__fmul_rn(dinv[r], (float)counts[j]), dinv[c]);
+    coo_rows[j] = r;
+    coo_cols[j] = c;
+    vals[j] = v;
+    edges[j] = (lgcn_edge_t)(((uint64_t)__float_as_uint(v) << 32) | (uint32_t)c);
+}
+
+// ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
 inline int herr(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
@@ -817,6 +850,70 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
     if (nnz == 0 || n_rows == 0) return 0;
     hipLaunchKernelGGL(k_csr_symmetric, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)), dim3(kBlock),
                        0, S(stream), rowptr, edges, n_rows, nnz, asym);
+    return last_err();
+}
+
+int lgcn_adj_degree(const int64_t* rows, int64_t n_edges, int32_t n, int32_t* deg,
+                    void* stream) {
+    if (n_edges < 0 || n < 0 || (n_edges > 0 && !rows) || (n > 0 && !deg)) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (n > 0) {
+        if (int e = herr(hipMemsetAsync(deg, 0, sizeof(int32_t) * (size_t)n, s))) return e;
+    }
+    if (n_edges == 0) return 0;
+    hipLaunchKernelGGL(k_adj_degree, dim3((uint32_t)((n_edges + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, s, rows, n_edges, deg);
+    return last_err();
+}
+
+int lgcn_adj_sort_unique(const int64_t* rows, const int64_t* cols, int64_t n_edges, int32_t n,
+                         uint64_t* keys_a, uint64_t* keys_b, uint64_t* uniq, int32_t* counts,
+                         int32_t* n_unique, void* temp, size_t* temp_bytes_host, void* stream) {
+    if (n_edges < 0 || n_edges > 0x7fffffffLL || n < 0 || !temp_bytes_host) return LGCN_EINVAL;
+    const uint64_t nn = (uint64_t)n * (uint64_t)n;
+    int end_bit = 1;
+    while (end_bit < 64 && (1ULL << end_bit) < nn) ++end_bit;
+    hipStream_t s = S(stream);
+    const int ne = (int)n_edges;
+    if (temp == nullptr) {
+        size_t b1 = 0, b2 = 0;
+        hipError_t e = hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys_a, keys_b, ne, 0,
+                                                         end_bit, s);
+        if (e != hipSuccess) return (int)e;
+        e = hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, keys_b, uniq, counts, n_unique, ne, s);
+        *temp_bytes_host = b1 > b2 ? b1 : b2;
+        return herr(e);
+    }
+    if (!rows || !cols || !keys_a || !keys_b || !uniq || !counts || !n_unique) return LGCN_EINVAL;
+    if (n_edges == 0) return herr(hipMemsetAsync(n_unique, 0, sizeof(int32_t), s));
+    hipLaunchKernelGGL(k_adj_keys, dim3((uint32_t)((n_edges + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, s, rows, cols, n_edges, (int64_t)n, keys_a);
+    if (int e = last_err()) return e;
+    size_t bytes = *temp_bytes_host;
+    if (int e = herr(hipcub::DeviceRadixSort::SortKeys(temp, bytes, keys_a, keys_b, ne, 0,
+                                                       end_bit, s)))
+        return e;
+    bytes = *temp_bytes_host;
+    return herr(hipcub::DeviceRunLengthEncode::Encode(temp, bytes, keys_b, uniq, counts, n_unique,
+                                                      ne, s));
+}
+
+int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, int32_t n,
+                    const float* dinv, int64_t* coo_rows, int64_t* coo_cols, float* vals,
+                    int32_t* rowptr, lgcn_edge_t* edges, void* stream) {
+    if (nnz < 0 || nnz > 0x7fffffffLL || n < 0 || !rowptr) return LGCN_EINVAL;
+    if (nnz > 0 && (!uniq || !counts || !dinv || !coo_rows || !coo_cols || !vals || !edges))
+        return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (nnz > 0) {
+        hipLaunchKernelGGL(k_adj_finish, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, uniq, counts, nnz, (int64_t)n, dinv, coo_rows, coo_cols, vals,
+                           edges);
+        if (int e = last_err()) return e;
+    }
+    const int64_t nr = (int64_t)n + 1;
+    hipLaunchKernelGGL(k_csr_rowptr, dim3((uint32_t)((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, coo_rows, nullptr, nnz, n, rowptr);
     return last_err();
 }
 

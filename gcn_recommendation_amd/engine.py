@@ -62,6 +62,10 @@ ABI = [
     ("lgcn_coo_sort_perm", ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P,
                                           ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
+    ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),
+    ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
+                                            ctypes.POINTER(ctypes.c_size_t), _P]),
+    ("lgcn_adj_finish", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
     ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, RowsT, _P, _I64, _I32,
                                        ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _P, _P, _I64, _I32,
@@ -252,6 +256,41 @@ def _coo_to_csr(lib, key, other, vals, nnz, n_keys, device, stream, sort):
     return rowptr, edges
 
 
+def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, cols_sorted):
+    """Attach the backward operator: Â itself if bitwise symmetric, else a stably sorted Âᵀ."""
+    g = Graph(n, n, rowptr, edges, nnz, device)
+    symmetric = False
+    if cols_sorted:
+        asym = torch.zeros(1, dtype=torch.int32, device=device)
+        _check(lib.lgcn_csr_check_symmetric(_ptr(rowptr), _ptr(edges), n, nnz, _ptr(asym),
+                                            stream), "lgcn_csr_check_symmetric")
+        symmetric = int(asym.item()) == 0
+    g.symmetric = symmetric
+    if symmetric:
+        g.transpose = g
+    else:
+        # Âᵀ with each row's entries in Â's stored order (torch's sparse t() + addmm loop)
+        t_rowptr, t_edges = _coo_to_csr(lib, cols, rows, vals, nnz, n, device, stream, sort=True)
+        g.transpose = Graph(n, n, t_rowptr, t_edges, nnz, device)
+        g.transpose.transpose = g
+    return g
+
+
+def _cache_key(adj):
+    idx, vals = adj._indices(), adj._values()
+    return (idx.data_ptr(), vals.data_ptr(), idx._version, vals._version, adj._nnz(),
+            tuple(adj.shape), str(adj.device))
+
+
+def attach_graph(adj, g):
+    """Cache a prepared Graph on the adjacency tensor it was built from."""
+    try:
+        adj._lgcn_graph = (_cache_key(adj), g)
+    except (AttributeError, RuntimeError):
+        pass
+    return adj
+
+
 def graph_from_coo(adj):
     """Convert the caller-owned sparse COO Â (main.py:334-336) into the engine's CSR, once.
 
@@ -266,8 +305,7 @@ def graph_from_coo(adj):
         raise LgcnError(f"adj_mat must be float32, got {adj.dtype}")
     idx = adj._indices()
     vals = adj._values()
-    key = (idx.data_ptr(), vals.data_ptr(), idx._version, vals._version, adj._nnz(),
-           tuple(adj.shape), str(adj.device))
+    key = _cache_key(adj)
     cached = getattr(adj, "_lgcn_graph", None)
     if cached is not None and cached[0] == key:
         return cached[1]
@@ -290,22 +328,8 @@ def graph_from_coo(adj):
             raise LgcnError("adj_mat has indices out of range")
         rowptr, edges = _coo_to_csr(lib, rows, cols, vals, nnz, n, device, stream,
                                     sort=bool(f & COO_ROWS_UNSORTED))
-        g = Graph(n, n, rowptr, edges, nnz, device)
-        symmetric = False
-        if not (f & (COO_ROWS_UNSORTED | COO_COLS_UNSORTED)):
-            asym = torch.zeros(1, dtype=torch.int32, device=device)
-            _check(lib.lgcn_csr_check_symmetric(_ptr(rowptr), _ptr(edges), n, nnz, _ptr(asym),
-                                                stream), "lgcn_csr_check_symmetric")
-            symmetric = int(asym.item()) == 0
-        g.symmetric = symmetric
-        if symmetric:
-            g.transpose = g
-        else:
-            # Âᵀ with each row's entries in Â's stored order (torch's sparse t() + addmm loop)
-            t_rowptr, t_edges = _coo_to_csr(lib, cols, rows, vals, nnz, n, device, stream,
-                                            sort=True)
-            g.transpose = Graph(n, n, t_rowptr, t_edges, nnz, device)
-            g.transpose.transpose = g
+        g = _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream,
+                          cols_sorted=not (f & (COO_ROWS_UNSORTED | COO_COLS_UNSORTED)))
     try:
         adj._lgcn_graph = (key, g)
     except (AttributeError, RuntimeError):

@@ -54,6 +54,69 @@ def build_norm_adj(train_user, train_item, U, I, B, ib_item=None, ib_brand=None,
     return torch.sparse_coo_tensor(idx, torch.from_numpy(v), torch.Size((n, n))).to(device)
 
 
+def build_norm_adj_device(train_user, train_item, U, I, B, ib_item=None, ib_brand=None,
+                          use_brand=True, device="cuda"):
+    """main.py:282-336 on the HIP device: the same `norm_adj_tensor`
+    (bitwise: stored order, duplicate merge, fp32 values) as build_norm_adj, plus the engine's
+    CSR plan attached to it, so the first model call does no conversion.
+
+    Device work: degree histogram (integer atomics), 64-bit radix sort of row*n+col keys,
+    run-length encode (multiplicity m), values fp32((d_r*m)*d_c), COO + CSR in one pass.
+    Host work: the edge-list concat (main.py:300-311) and d = rowsum^-1/2 with numpy's float32
+    power (main.py:326-329) — numpy's power is not correctly rounded, so only numpy reproduces
+    the reference's d bitwise; it is N floats, the rest is O(nnz) on the device.
+    """
+    import ctypes
+    from . import engine
+    lib = engine.load_library()
+    dev = torch.device(device)
+    n = U + I + B
+    rows, cols = edge_lists(train_user, train_item, U, I, ib_item, ib_brand, use_brand)
+    ne = int(rows.size)
+    if n > engine.INT32_MAX - 1 or ne > engine.INT32_MAX:
+        raise engine.LgcnError("graph too large for int32 CSR")
+    P = engine._ptr
+    with torch.cuda.device(dev):
+        st = engine._stream(dev)
+        r_d = torch.from_numpy(rows).to(dev)
+        c_d = torch.from_numpy(cols).to(dev)
+        deg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        engine._check(lib.lgcn_adj_degree(P(r_d), ne, n, P(deg), st), "lgcn_adj_degree")
+        rowsum = deg[:n].cpu().numpy().astype(np.float32)
+        with np.errstate(divide="ignore"):
+            dinv = np.power(rowsum, np.float32(-0.5))
+        dinv[np.isinf(dinv)] = np.float32(0.0)
+        dinv_d = torch.from_numpy(dinv).to(dev)
+        m = max(ne, 1)
+        keys_a = torch.empty(m, dtype=torch.int64, device=dev)
+        keys_b = torch.empty(m, dtype=torch.int64, device=dev)
+        uniq = torch.empty(m, dtype=torch.int64, device=dev)
+        counts = torch.empty(m, dtype=torch.int32, device=dev)
+        n_unique = torch.zeros(1, dtype=torch.int32, device=dev)
+        nbytes = ctypes.c_size_t(0)
+        engine._check(lib.lgcn_adj_sort_unique(P(r_d), P(c_d), ne, n, P(keys_a), P(keys_b),
+                                               P(uniq), P(counts), P(n_unique), None,
+                                               ctypes.byref(nbytes), st), "lgcn_adj_sort_unique")
+        temp = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
+        engine._check(lib.lgcn_adj_sort_unique(P(r_d), P(c_d), ne, n, P(keys_a), P(keys_b),
+                                               P(uniq), P(counts), P(n_unique), P(temp),
+                                               ctypes.byref(nbytes), st), "lgcn_adj_sort_unique")
+        del temp, keys_a, keys_b, r_d, c_d
+        nnz = int(n_unique.item())
+        idx = torch.empty((2, max(nnz, 1)), dtype=torch.int64, device=dev)
+        vals = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+        rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        edges = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+        engine._check(lib.lgcn_adj_finish(P(uniq), P(counts), nnz, n, P(dinv_d), P(idx[0]),
+                                          P(idx[1]), P(vals), P(rowptr), P(edges), st),
+                      "lgcn_adj_finish")
+        idx, vals = idx[:, :nnz], vals[:nnz]
+        adj = torch.sparse_coo_tensor(idx, vals, (n, n))
+        g = engine._finish_graph(lib, adj._indices()[0], adj._indices()[1], adj._values(), rowptr,
+                                 edges, n, nnz, dev, st, cols_sorted=True)
+    return engine.attach_graph(adj, g)
+
+
 # ----------------------------------------------------------------------------------------------
 # synthetic interactions (BASELINE.json configs; SURVEY §8d)
 # ----------------------------------------------------------------------------------------------

@@ -141,6 +141,27 @@ int lgcn_coo_sort_perm(const int64_t* keys, int64_t nnz, int32_t n_keys, int32_t
 int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
                              int64_t nnz, int32_t* asym, void* stream);
 
+/* ---- adjacency builder (main.py:313-336 on the device) -------------------------------------- */
+/* deg[r] = number of stored edges with row r (duplicates counted, main.py:326 rowsum of the
+ * ones matrix); zeroes deg itself. */
+int lgcn_adj_degree(const int64_t* rows, int64_t n_edges, int32_t n, int32_t* deg, void* stream);
+
+/* Sort keys row*n+col (64-bit radix) and run-length encode them: uniq[0..*n_unique) ascending
+ * (= (row, col) order), counts = duplicate multiplicity m. Two-call protocol for temp (temp ==
+ * NULL: only *temp_bytes_host). keys_a/keys_b/uniq: n_edges uint64; counts: n_edges int32;
+ * n_unique: one device int32. */
+int lgcn_adj_sort_unique(const int64_t* rows, const int64_t* cols, int64_t n_edges, int32_t n,
+                         uint64_t* keys_a, uint64_t* keys_b, uint64_t* uniq, int32_t* counts,
+                         int32_t* n_unique, void* temp, size_t* temp_bytes_host, void* stream);
+
+/* Values fp32((dinv[r] * m) * dinv[c]) (main.py:330-331 scipy D·A·D, each product rounded), the
+ * COO the reference hands to the model (int64 rows/cols, fp32 vals: main.py:334-336) and the
+ * engine's CSR (rowptr[n+1], edges[nnz]) in one pass. dinv = rowsum^-1/2 with inf -> 0, computed
+ * by the caller (numpy's float32 power, main.py:328, is reproduced bitwise only by numpy). */
+int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, int32_t n,
+                    const float* dinv, int64_t* coo_rows, int64_t* coo_cols, float* vals,
+                    int32_t* rowptr, lgcn_edge_t* edges, void* stream);
+
 /* ---- the propagation (models/lightgcn.py:44-54) -------------------------------------------- */
 
 /* One layer Y = epilogue(Â·X) over rows [0, n_rows):

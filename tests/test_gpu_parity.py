@@ -291,3 +291,34 @@ def test_dist_rowpart_and_featsplit_kernels_on_gpu(gpu_device):
         sl, _ = D.featsplit_slices(segs, P, p)
         cols.append(D.featsplit_forward(g, sl, K, thr).cpu().numpy())
     assert np.array_equal(np.concatenate(cols, 1), want)
+
+
+@pytest.mark.parametrize("name", CASES + ["c1_fusion"])
+def test_device_adjacency_builder_bitwise(gpu_device, name):
+    """graph.build_norm_adj_device == the reference-built Â (main.py:282-336), bitwise, and its
+    attached CSR plan gives the same propagation as a plan built from that COO."""
+    z = load_case(name)
+    U, I, B, d, K = case_dims(z)
+    adj = graph.build_norm_adj_device(z["train_user"], z["train_item"], U, I, B, z["ib_item"],
+                                      z["ib_brand"], bool(z["use_brand"]), device=gpu_device)
+    idx = adj._indices().cpu().numpy()
+    np.testing.assert_array_equal(idx[0], z["adj_row"])
+    np.testing.assert_array_equal(idx[1], z["adj_col"])
+    assert np.array_equal(adj._values().cpu().numpy().view(np.uint32),
+                          z["adj_val"].view(np.uint32))
+    g = engine.graph_from_coo(adj)            # the attached plan is reused
+    assert g is adj._lgcn_graph[1]
+    e0 = torch.from_numpy(case_e0(z)).to(gpu_device) if name != "c1_fusion" else \
+        torch.from_numpy(z["full/E0"]).to(gpu_device)
+    got = engine.propagate_forward(g, [e0], K, hub_threshold=engine.INT32_MAX).cpu().numpy()
+    assert sha1(got) == str(z["sha1/final"])
+
+
+def test_device_adjacency_builder_c2_powerlaw(gpu_device):
+    u, i = graph.powerlaw_interactions(50_000, 50_000, 1_000_000, 2)
+    ref = graph.build_norm_adj(u, i, 50_000, 50_000, 0, use_brand=False)
+    adj = graph.build_norm_adj_device(u, i, 50_000, 50_000, 0, use_brand=False, device=gpu_device)
+    assert torch.equal(adj._indices().cpu(), ref._indices())
+    assert torch.equal(adj._values().cpu().view(torch.int32), ref._values().view(torch.int32))
+    g = engine.graph_from_coo(adj)
+    assert g.transpose is not None and (g.symmetric or g.transpose is not g)

@@ -47,7 +47,7 @@ def main():
     cfg = bench.CONFIGS[args.config]
     res = {}
     for gen in args.gens.split(","):
-        r, c, v, _, _ = bench.make_graph(cfg, gen, 16)
+        r, c, v, _, _, _ = bench.make_graph(cfg, gen, 16)
         U, I = cfg["users"], cfg["items"]
         n = U + I
         adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack((r, c))), torch.from_numpy(v),
