@@ -6,7 +6,7 @@ import subprocess
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
-SRC = os.path.join(_PKG, "csrc", "lgcn_engine.hip")
+SRCS = [os.path.join(_PKG, "csrc", f) for f in ("lgcn_engine.hip", "lgcn_eval.hip")]
 HDR = os.path.join(ROOT, "include", "lgcn.h")
 OUT = os.path.join(_PKG, "liblgcn_engine.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
@@ -23,15 +23,15 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in SRCS + [HDR, __file__])
 
 
 def build(force=False, verbose=False):
     if not force and not needs_build():
         return OUT
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-I", os.path.join(ROOT, "include"), SRC,
-           "-o", OUT + ".tmp"]
+           "-ffp-contract=off", "-Wall", "-I", os.path.join(ROOT, "include")] + SRCS + \
+          ["-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -41,3 +41,77 @@ def recall_ndcg(user_emb, item_emb, users, heldout_items, train_rowptr, train_co
     if return_topk:
         return float(np.mean(hits)), float(np.mean(ndcgs)), np.concatenate(tops)
     return float(np.mean(hits)), float(np.mean(ndcgs))
+
+
+# ----------------------------------------------------------------------------------------------
+# fused path: lgcn_score_topk (score GEMM + train mask + top-K in one kernel, no score matrix)
+# ----------------------------------------------------------------------------------------------
+def mask_csr(users, items, n_users):
+    """Sorted, de-duplicated per-user item lists (the train_user_items dict of main.py:407)."""
+    users = np.asarray(users, dtype=np.int64)
+    items = np.asarray(items, dtype=np.int64)
+    key = np.unique(users * (items.max(initial=0) + 1) + items) if users.size else users
+    if users.size:
+        span = items.max(initial=0) + 1
+        u, it = key // span, key % span
+    else:
+        u, it = users, items
+    rowptr = np.searchsorted(u, np.arange(n_users + 1)).astype(np.int32)
+    return rowptr, it.astype(np.int32)
+
+
+def topk_fused(user_emb, item_emb, users, mask_rowptr, mask_items, k=20):
+    """Top-k items per user (scores, indices) with the train items masked to -1e10.
+    user_emb [U x d], item_emb [I x d] fp32 on the HIP device; users: int32/int64 ids."""
+    import ctypes
+    from . import engine
+    lib = engine.load_library()
+    dev = item_emb.device
+    d = item_emb.shape[1]
+    users = torch.as_tensor(users, device=dev).to(torch.int32).contiguous()
+    n = int(users.numel())
+    ue, ie = user_emb.contiguous(), item_emb.contiguous()
+    mrow = torch.as_tensor(mask_rowptr, device=dev).to(torch.int32).contiguous()
+    mit = torch.as_tensor(mask_items, device=dev).to(torch.int32).contiguous()
+    if mit.numel() == 0:
+        mit = torch.zeros(1, dtype=torch.int32, device=dev)
+    n_cu = ctypes.c_int32(0)
+    engine._check(lib.lgcn_device_info(dev.index or 0, ctypes.byref(n_cu), None), "device_info")
+    splits = lib.lgcn_eval_splits(n, int(ie.shape[0]), n_cu.value)
+    part_s = torch.empty((splits, max(n, 1), k), dtype=torch.float32, device=dev)
+    part_i = torch.empty((splits, max(n, 1), k), dtype=torch.int32, device=dev)
+    top_s = torch.empty((max(n, 1), k), dtype=torch.float32, device=dev)
+    top_i = torch.empty((max(n, 1), k), dtype=torch.int32, device=dev)
+    P = engine._ptr
+    with torch.cuda.device(dev):
+        engine._check(lib.lgcn_score_topk(P(ue), ue.stride(0), P(users), n, P(ie), ie.stride(0),
+                                          int(ie.shape[0]), d, P(mrow), P(mit), k, splits,
+                                          P(part_s), P(part_i), P(top_s), P(top_i),
+                                          engine._stream(dev)), "lgcn_score_topk")
+    return top_s[:n], top_i[:n]
+
+
+def evaluate(model, val_or_test_data, train_data, norm_adj_tensor, k, device, batch_size=8192,
+             use_brand=True, item_brand_df=None):
+    """main.py:404-439 (same signature and metrics) on the fused kernel: one propagation, then
+    per batch of users one lgcn_score_topk launch; hit -> recall 1, NDCG = 1/log2(pos + 2)."""
+    model.eval()
+    test_user_items = dict(zip(val_or_test_data["user_idx"], val_or_test_data["item_idx"]))
+    test_users = np.fromiter(test_user_items.keys(), dtype=np.int64, count=len(test_user_items))
+    truth = np.fromiter(test_user_items.values(), dtype=np.int64, count=len(test_user_items))
+    with torch.no_grad():
+        all_user_emb, all_item_emb, _, _, _ = model(norm_adj_tensor)
+        mrow, mit = mask_csr(train_data["user_idx"].to_numpy(), train_data["item_idx"].to_numpy(),
+                             all_user_emb.shape[0])
+        tops = []
+        for s in range(0, len(test_users), batch_size):
+            _, ti = topk_fused(all_user_emb, all_item_emb, test_users[s:s + batch_size], mrow,
+                               mit, k)
+            tops.append(ti.cpu().numpy())
+    top = np.concatenate(tops) if tops else np.zeros((0, k), np.int32)
+    hit = top == truth[:, None]
+    found = hit.any(1)
+    pos = hit.argmax(1)
+    ndcg = np.where(found, 1.0 / np.log2(pos + 2), 0.0)
+    return float(found.mean()) if len(found) else float("nan"), \
+        float(ndcg.mean()) if len(found) else float("nan")

@@ -204,6 +204,22 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int
                             int32_t d, int32_t K, float* work_c, float* work_h, float* grad_e0,
                             void* stream);
 
+/* ---- evaluation (main.py:404-439) ----------------------------------------------------------- */
+/* Item splits for lgcn_score_topk: ~2 blocks per CU, >= 2048 items per split, <= 256. */
+int lgcn_eval_splits(int32_t n_users, int32_t n_items, int32_t n_cu);
+
+/* Fused score + train-item mask + top-k for a batch of users (main.py:420-426) without the
+ * [n_users x n_items] score matrix: scores = user_emb[users[b]] · item_emb[i] (exact-f32 MFMA,
+ * an ordered fmaf chain), items of user u listed in mask_items[mask_rowptr[u]:mask_rowptr[u+1]]
+ * (sorted ascending) score -1e10, ties broken by lower item index. Outputs top_scores/top_idx
+ * [n_users x k] in rank order (-inf / -1 past n_items). d in {64, 128}, k in [1, 32], 16-B
+ * aligned rows. part_scores/part_idx: scratch [n_splits x n_users x k]. */
+int lgcn_score_topk(const float* user_emb, int64_t ld_u, const int32_t* users, int32_t n_users,
+                    const float* item_emb, int64_t ld_i, int32_t n_items, int32_t d,
+                    const int32_t* mask_rowptr, const int32_t* mask_items, int32_t k,
+                    int32_t n_splits, float* part_scores, int32_t* part_idx, float* top_scores,
+                    int32_t* top_idx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
