@@ -71,10 +71,17 @@ __device__ __forceinline__ int2 load_edge(const lgcn_edge_t* e) {
 
 // Sequential fmaf chain over edge records [beg, end) — the ATen CPU order (one row's nonzeros in
 // stored order, y = fma(val, x, y) starting from +0). U gathers are in flight before the folds.
-template <typename V, int G, int NV, int U>
+template <typename V, bool XD>
+__device__ __forceinline__ V load_x(const float* p, float xdiv) {
+    const V v = VT<V>::load(p);
+    if constexpr (XD) return VT<V>::div(v, xdiv);  // gathered operand = X / xdiv, rounded once
+    else return v;
+}
+
+template <typename V, int G, int NV, int U, bool XD = false>
 __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges, int32_t beg,
                                            int32_t end, const lgcn_rows_t& x, int lane, int dW,
-                                           V (&acc)[NV]) {
+                                           V (&acc)[NV], float xdiv = 1.f) {
     using T = VT<V>;
     for (int32_t j = beg; j < end; j += U) {
         const int n = min(U, end - j);
@@ -88,7 +95,7 @@ __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int c = lane + q * G;
-                xv[u][q] = (u < n && c < dW) ? T::load(rp + c * T::W) : T::zero();
+                xv[u][q] = (u < n && c < dW) ? load_x<V, XD>(rp + c * T::W, xdiv) : T::zero();
             }
         }
 #pragma unroll
@@ -122,7 +129,8 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
             s = T::add(s, out);
             out = T::div(s, ep.div);
         } else if constexpr (MODE == LGCN_EPI_ADD) {
-            out = T::add(T::load(ep.addend + (int64_t)row * ep.ld_add + c * T::W), out);
+            // Horner step: (Z / div) + Â·X, Z read in place (segments), Z / div rounded once
+            out = T::add(T::div(T::load(seg_row(ep.addend, row) + c * T::W), ep.div), out);
         }
         T::store(yr + c * T::W, out);
     }
@@ -136,12 +144,12 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
 //    record wb+l) with the next window prefetched, and reach every lane by shuffles — the only
 //    memory latency left on the critical path is the gather itself;
 //  * U gathers are in flight per group across row boundaries.
-template <typename V, int G, int NV, int MODE, int RPG, int U>
+template <typename V, int G, int NV, int MODE, int RPG, int U, bool XD>
 __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                                             const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
                                             int32_t hub_thr, int32_t r0, const lgcn_rows_t& x,
                                             float* __restrict__ y, int64_t ldy, int lane, int dW,
-                                            const lgcn_epilogue_t& ep) {
+                                            const lgcn_epilogue_t& ep, float xdiv) {
     using T = VT<V>;
     static_assert(RPG < G, "row boundaries are held one per lane");
     const int nrows = min(RPG, n_rows - r0);
@@ -212,7 +220,7 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int c = lane + q * G;
-                xv[u][q] = (u < cnt && c < dW) ? T::load(rp + c * T::W) : T::zero();
+                xv[u][q] = (u < cnt && c < dW) ? load_x<V, XD>(rp + c * T::W, xdiv) : T::zero();
             }
         }
 #pragma unroll
@@ -246,12 +254,12 @@ __device__ __forceinline__ void mean_prefetch(const lgcn_epilogue_t& ep, int32_t
     }
 }
 
-template <typename V, int G, int NV, int MODE, int RPG, int U, int NP = 0>
+template <typename V, int G, int NV, int MODE, int RPG, int U, int NP = 0, bool XD = false>
 __global__ __launch_bounds__(kBlock) void k_layer(
     const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
     int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
     int32_t hub_blocks, float* __restrict__ partials, lgcn_rows_t x, float* __restrict__ y,
-    int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep) {
+    int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep, float xdiv) {
     using T = VT<V>;
     constexpr int RPB = kBlock / G;
     const int lane = threadIdx.x & (G - 1);
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
         constexpr int UH = NV >= 8 ? 1 : 8 / NV;  // hub chunks are long: deep unroll
-        accumulate<V, G, NV, UH>(edges, w.beg, w.end, x, lane, dW, acc);
+        accumulate<V, G, NV, UH, XD>(edges, w.beg, w.end, x, lane, dW, acc, xdiv);
         float* pr = partials + (int64_t)w.slot * d;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
         if constexpr (MODE == LGCN_EPI_MEAN && NP > 0) {
             V pre[NP][NV];
             mean_prefetch<V, G, NV, NP>(ep, row, lane, dW, pre);
-            accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
+            accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv);
             float* yr = y + (int64_t)row * ldy;
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
@@ -299,14 +307,14 @@ __global__ __launch_bounds__(kBlock) void k_layer(
                 T::store(yr + c * T::W, T::div(T::add(s, acc[q]), ep.div));
             }
         } else {
-            accumulate<V, G, NV, U>(edges, beg, end, x, lane, dW, acc);
+            accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv);
             epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
         }
     } else {
         const int64_t r0 = gidx * RPG;
         if (r0 >= n_rows) return;
-        rows_bundle<V, G, NV, MODE, RPG, U>(rowptr, edges, n_rows, hub_thr, (int32_t)r0, x, y, ldy,
-                                            lane, dW, ep);
+        rows_bundle<V, G, NV, MODE, RPG, U, XD>(rowptr, edges, n_rows, hub_thr, (int32_t)r0, x, y,
+                                                ldy, lane, dW, ep, xdiv);
     }
 }
 
@@ -453,10 +461,23 @@ __global__ void k_csr_symmetric(const int32_t* __restrict__ rowptr,
 // adjacency builder (main.py:313-336 on the device): degree histogram, duplicate merge by a
 // 64-bit radix sort of row*n+col keys + run-length encode, values fp32((d_r * m) * d_c)
 // ---------------------------------------------------------------------------------------------
-__global__ void k_adj_degree(const int64_t* __restrict__ rows, int64_t n_edges,
+// deg[r] = (first sorted key >= (r+1)*n) - (first sorted key >= r*n): raw edges of row r,
+// duplicates included; binary search, no atomics (a 2.77M-degree hub made atomics serialise)
+__global__ void k_adj_degree(const uint64_t* __restrict__ keys, int64_t n_edges, int64_t n,
                              int32_t* __restrict__ deg) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n_edges) atomicAdd(deg + rows[j], 1);  // integer adds: order-independent
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    int64_t b[2];
+    for (int t = 0; t < 2; ++t) {
+        const uint64_t target = (uint64_t)(r + t) * (uint64_t)n;
+        int64_t lo = 0, hi = n_edges;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < target) lo = mid + 1; else hi = mid;
+        }
+        b[t] = lo;
+    }
+    deg[r] = (int32_t)(b[1] - b[0]);
 }
 
 __global__ void k_adj_keys(const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
@@ -527,7 +548,7 @@ bool epi_aligned(const lgcn_epilogue_t& ep) {
         for (int i = 0; i + 1 < ep.n_prev; ++i)
             if (!al16(ep.prev_dense[i])) return false;
     }
-    if (ep.mode == LGCN_EPI_ADD && (!al16(ep.addend) || ep.ld_add % 4)) return false;
+    if (ep.mode == LGCN_EPI_ADD && !rows_aligned(ep.addend)) return false;
     return true;
 }
 
@@ -540,7 +561,7 @@ template <typename V, int G, int NV, int RPG, int U, int NP = 0>
 int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
                      const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                      const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
-                     const lgcn_epilogue_t& ep, hipStream_t s) {
+                     const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
     constexpr int RPB = kBlock / G;
     const int32_t hub_blocks = (n_items + RPB - 1) / RPB;
     const int64_t row_groups = ((int64_t)n_rows + RPG - 1) / RPG;
@@ -550,19 +571,27 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_
     if (grid > 0x7fffffffLL) return LGCN_EINVAL;
     switch (ep.mode) {
         case LGCN_EPI_STORE:
+            if (xdiv != 1.f) return LGCN_EINVAL;  // gather scaling exists for the backward only
             hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_STORE, RPG, U>), dim3((uint32_t)grid),
                                dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
-                               hub_blocks, partials, x, y, ldy, d, dW, ep);
+                               hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         case LGCN_EPI_MEAN:
+            if (xdiv != 1.f) return LGCN_EINVAL;
             hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN, RPG, U, NP>), dim3((uint32_t)grid),
                                dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
-                               hub_blocks, partials, x, y, ldy, d, dW, ep);
+                               hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         case LGCN_EPI_ADD:
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U>), dim3((uint32_t)grid),
-                               dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
-                               hub_blocks, partials, x, y, ldy, d, dW, ep);
+            if (xdiv != 1.f)
+                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, true>),
+                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
+                                   thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
+                                   xdiv);
+            else
+                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U>), dim3((uint32_t)grid),
+                                   dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                                   hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         default:
             return LGCN_EINVAL;
@@ -574,13 +603,13 @@ template <typename V, int G, int NV>
 int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
                    const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                    const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
-                   const lgcn_epilogue_t& ep, hipStream_t s) {
+                   const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
     // one row per group (deep unroll) for the MEAN epilogue, whose reads of E0..E_{K-1} would
     // otherwise serialise inside a row stream; row bundles (shallow unroll) everywhere else
     constexpr int U1 = NV >= 8 ? 1 : 8 / NV;
     constexpr int UB = NV >= 4 ? 1 : 4 / NV;
     constexpr int RB = G >= 16 ? 15 : G - 1;
-#define LGCN_ARGS rowptr, edges, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, s
+#define LGCN_ARGS rowptr, edges, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, xdiv, s
     if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: explicit variants (lgcn_tune)
 #define LGCN_V(R_, U_) \
         if (g_rows_per_group == R_ && g_unroll == U_) return launch_layer_rpg<V, G, NV, R_, U_>(LGCN_ARGS);
@@ -674,17 +703,17 @@ int check_epi(const lgcn_epilogue_t* ep) {
         if (ep->n_prev - 1 > LGCN_MAX_LAYERS) return LGCN_ETOOMANY;
         if (!(ep->div > 0.f)) return LGCN_EINVAL;
     }
-    if (ep->mode == LGCN_EPI_ADD && !ep->addend) return LGCN_EINVAL;
+    if (ep->mode == LGCN_EPI_ADD && (!ep->addend.p0 || !(ep->div > 0.f))) return LGCN_EINVAL;
     return 0;
 }
 
 struct LayerF {
     const int32_t* rowptr; const lgcn_edge_t* edges; int32_t n_rows, thr;
     const lgcn_hub_item_t* items; int32_t n_items; float* partials; const lgcn_rows_t* x;
-    float* y; int64_t ldy; int32_t d, dW; const lgcn_epilogue_t* ep; hipStream_t s;
+    float* y; int64_t ldy; int32_t d, dW; const lgcn_epilogue_t* ep; float xdiv; hipStream_t s;
     template <typename V, int G, int NV> int operator()() const {
         return launch_layer_t<V, G, NV>(rowptr, edges, n_rows, thr, items, n_items, partials, *x,
-                                        y, ldy, d, dW, *ep, s);
+                                        y, ldy, d, dW, *ep, xdiv, s);
     }
 };
 
@@ -705,11 +734,13 @@ struct ScaleF {
 
 int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
                const lgcn_hub_item_t* items, int32_t n_items, float* partials, lgcn_rows_t x,
-               float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+               float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, float xdiv,
+               hipStream_t s) {
     const bool vec_ok = rows_aligned(x) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep) &&
                         (n_items == 0 || al16(partials));
     const Geo g = pick_geo(d, vec_ok);
-    LayerF f{rowptr, edges, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW, &ep, s};
+    LayerF f{rowptr, edges, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW, &ep,
+             xdiv, s};
     return dispatch_geo(g, f);
 }
 
@@ -853,16 +884,13 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
     return last_err();
 }
 
-int lgcn_adj_degree(const int64_t* rows, int64_t n_edges, int32_t n, int32_t* deg,
+int lgcn_adj_degree(const uint64_t* keys_sorted, int64_t n_edges, int32_t n, int32_t* deg,
                     void* stream) {
-    if (n_edges < 0 || n < 0 || (n_edges > 0 && !rows) || (n > 0 && !deg)) return LGCN_EINVAL;
-    hipStream_t s = S(stream);
-    if (n > 0) {
-        if (int e = herr(hipMemsetAsync(deg, 0, sizeof(int32_t) * (size_t)n, s))) return e;
-    }
-    if (n_edges == 0) return 0;
-    hipLaunchKernelGGL(k_adj_degree, dim3((uint32_t)((n_edges + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, s, rows, n_edges, deg);
+    if (n_edges < 0 || n < 0 || (n_edges > 0 && !keys_sorted) || (n > 0 && !deg))
+        return LGCN_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_adj_degree, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       S(stream), keys_sorted, n_edges, (int64_t)n, deg);
     return last_err();
 }
 
@@ -919,14 +947,15 @@ int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, in
 
 int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
                     int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
-                    float* partials, lgcn_rows_t x, float* y, int64_t ldy, int32_t d,
+                    float* partials, lgcn_rows_t x, float x_div, float* y, int64_t ldy, int32_t d,
                     const lgcn_epilogue_t* epi_host, void* stream) {
     if (int e = valid_geom(n_rows, d)) return e;
     if (int e = check_epi(epi_host)) return e;
     if (n_rows > 0 && (!rowptr || !y || ldy < d)) return LGCN_EINVAL;
     if (n_hub_items < 0 || (n_hub_items > 0 && (!hub_items || !partials))) return LGCN_EINVAL;
+    if (!(x_div > 0.f)) return LGCN_EINVAL;
     return spmm_layer(rowptr, edges, n_rows, hub_threshold, hub_items, n_hub_items, partials, x, y,
-                      ldy, d, *epi_host, S(stream));
+                      ldy, d, *epi_host, x_div, S(stream));
 }
 
 int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
@@ -977,7 +1006,7 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int3
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1)], s))) return e;
         }
         if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials, x,
-                               y, d, d, ep, s))
+                               y, d, d, ep, 1.f, s))
             return e;
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1) + 1], s))) return e;
@@ -990,30 +1019,31 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int3
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, float* partials, const float* grad_out,
-                            int32_t d, int32_t K, float* work_c, float* work_h, float* grad_e0,
-                            void* stream) {
+                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out, int32_t d,
+                            int32_t K, float* work_h, float* grad_e0, void* stream) {
     if (int e = valid_geom(n, d)) return e;
-    if (K < 0 || !grad_out || !grad_e0) return LGCN_EINVAL;
+    if (K < 0 || !grad_out.p0 || !grad_e0) return LGCN_EINVAL;
     hipStream_t s = S(stream);
-    const lgcn_rows_t g = dense_rows(grad_out, n, d);
-    if (K == 0) return scale_rows(g, n, d, 1.0f, grad_e0, d, s);
-    if (!work_c || (K > 1 && !work_h)) return LGCN_EINVAL;
-    // MeanBackward: every stacked layer receives G / (K+1)
-    if (int e = scale_rows(g, n, d, (float)(K + 1), work_c, d, s)) return e;
-    const float* h = work_c;
+    if (K == 0) return scale_rows(grad_out, n, d, 1.0f, grad_e0, d, s);
+    if (K > 1 && !work_h) return LGCN_EINVAL;
+    // MeanBackward hands every layer c = G / (K+1); it is never materialised: layer 1 gathers
+    // G / (K+1) on load and every epilogue adds G[row] / (K+1) (same rounding as c).
+    const float div = (float)(K + 1);
+    lgcn_epilogue_t ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.mode = LGCN_EPI_ADD;
+    ep.addend = grad_out;
+    ep.div = div;
+    lgcn_rows_t h = grad_out;
+    float xdiv = div;
     for (int k = 1; k <= K; ++k) {
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
-        lgcn_epilogue_t ep;
-        memset(&ep, 0, sizeof(ep));
-        ep.mode = LGCN_EPI_ADD;
-        ep.addend = work_c;
-        ep.ld_add = d;
-        if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials,
-                               dense_rows(h, n, d), y, d, d, ep, s))
+        if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials, h,
+                               y, d, d, ep, xdiv, s))
             return e;
         if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;
-        h = y;
+        h = dense_rows(y, n, d);
+        xdiv = 1.f;
     }
     return 0;
 }

@@ -40,7 +40,7 @@ class EpilogueT(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("n_prev", ctypes.c_int32), ("div", ctypes.c_float),
                 ("pad", ctypes.c_int32), ("prev0", RowsT),
                 ("prev_dense", ctypes.c_void_p * LGCN_MAX_LAYERS), ("ld_prev", ctypes.c_int64),
-                ("addend", ctypes.c_void_p), ("ld_add", ctypes.c_int64)]
+                ("addend", RowsT)]
 
 
 class LgcnError(RuntimeError):
@@ -62,22 +62,22 @@ ABI = [
     ("lgcn_coo_sort_perm", ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P,
                                           ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
-    ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),
+    ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),  # (sorted keys, ...)
     ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
                                             ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_adj_finish", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
     ("lgcn_eval_splits", ctypes.c_int, [_I32, _I32, _I32]),
     ("lgcn_score_topk", ctypes.c_int, [_P, _I64, _P, _I32, _P, _I64, _I32, _I32, _P, _P, _I32,
                                        _I32, _P, _P, _P, _P, _P]),
-    ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, RowsT, _P, _I64, _I32,
-                                       ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, RowsT, ctypes.c_float,
+                                       _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _P, _P, _I64, _I32,
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
     ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, RowsT,
                                               _I32, _I32, _P, _P, _P, _P]),
-    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, _P,
-                                               _I32, _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, RowsT,
+                                               _I32, _I32, _P, _P, _P]),
 ]
 
 
@@ -343,7 +343,8 @@ def graph_from_coo(adj):
 # ----------------------------------------------------------------------------------------------
 # propagation
 # ----------------------------------------------------------------------------------------------
-def _epilogue(mode, prev0=None, prev_dense=(), ld_prev=0, div=1.0, addend=None, ld_add=0):
+def _epilogue(mode, prev0=None, prev_dense=(), ld_prev=0, div=1.0, addend=None):
+    """addend: an lgcn_rows_t (segments) for LGCN_EPI_ADD, added as addend / div."""
     ep = EpilogueT()
     ep.mode = mode
     ep.div = div
@@ -354,8 +355,7 @@ def _epilogue(mode, prev0=None, prev_dense=(), ld_prev=0, div=1.0, addend=None, 
             ep.prev_dense[i] = t.data_ptr()
         ep.ld_prev = ld_prev
     if addend is not None:
-        ep.addend = addend.data_ptr()
-        ep.ld_add = ld_add
+        ep.addend = addend
     return ep
 
 
@@ -369,8 +369,8 @@ def _check_emb(segments, d, device):
             raise LgcnError("embedding blocks must be contiguous [rows x d]")
 
 
-def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None):
-    """One layer Y = epilogue(Â·X) through lgcn_spmm_layer + lgcn_hub_combine."""
+def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0):
+    """One layer Y = epilogue(Â·(X / x_div)) through lgcn_spmm_layer + lgcn_hub_combine."""
     lib = load_library()
     hp = hubs or graph.hubs(hub_threshold)
     partials = None
@@ -380,8 +380,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     x = rows_desc(x_segments, d)
     _check(lib.lgcn_spmm_layer(_ptr(graph.rowptr), _ptr(graph.edges), graph.n_rows,
                                min(hp.threshold, INT32_MAX), _ptr(hp.items), hp.n_items,
-                               _ptr(partials), x, _ptr(y), y.stride(0), d, ctypes.byref(epi),
-                               stream), "lgcn_spmm_layer")
+                               _ptr(partials), x, x_div, _ptr(y), y.stride(0), d,
+                               ctypes.byref(epi), stream), "lgcn_spmm_layer")
     if hp.n_rows:
         _check(lib.lgcn_hub_combine(_ptr(hp.rows), hp.n_rows, _ptr(partials), _ptr(y), y.stride(0),
                                     d, ctypes.byref(epi), stream), "lgcn_hub_combine")
@@ -432,54 +432,74 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
 
 
 def propagate_backward(graph, grad_out, K, hub_threshold=None):
-    """dE0 = Σ_k (Âᵀ)^k G/(K+1), Horner order h = G/(K+1) + Âᵀ h (autograd's accumulation)."""
+    """dE0 = Σ_k (Âᵀ)^k G/(K+1), Horner order h = G/(K+1) + Âᵀ h (autograd's accumulation).
+
+    grad_out: the [n x d] upstream gradient, or a list of row blocks (the user / item / brand
+    output gradients, read in place). c = G/(K+1) is never materialised: layer 1 divides on
+    load and every epilogue adds G[row]/(K+1) — the same rounding as a stored c."""
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
     gt = graph.transpose
-    n, d = grad_out.shape
-    g = grad_out.contiguous()
+    segs = [t.contiguous() for t in grad_out] if isinstance(grad_out, (list, tuple)) \
+        else [grad_out.contiguous()]
+    d = segs[0].shape[1]
+    n = sum(int(t.shape[0]) for t in segs)
+    _check_emb(segs, d, graph.device)
     lib = load_library()
     dev = graph.device
     with torch.cuda.device(dev):
         stream = _stream(dev)
+        g = rows_desc(segs, d)
         out = torch.empty((n, d), dtype=torch.float32, device=dev)
         if K == 0:
-            _check(lib.lgcn_scale_rows(rows_desc([g], d), n, d, 1.0, _ptr(out), d, stream),
-                   "lgcn_scale_rows")
+            _check(lib.lgcn_scale_rows(g, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
             return out
-        c = torch.empty((n, d), dtype=torch.float32, device=dev)
-        _check(lib.lgcn_scale_rows(rows_desc([g], d), n, d, float(K + 1), _ptr(c), d, stream),
-               "lgcn_scale_rows")
         hp = gt.hubs(hub_threshold)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
-        h = c
-        ep = _epilogue(LGCN_EPI_ADD, addend=c, ld_add=d)
+        ep = _epilogue(LGCN_EPI_ADD, addend=g, div=float(K + 1))
+        h = segs
         for k in range(1, K + 1):
             y = out if (K - k) % 2 == 0 else work
-            spmm_layer(gt, [h], y, d, ep, hub_threshold, hp, stream)
-            h = y
+            spmm_layer(gt, h, y, d, ep, hub_threshold, hp, stream,
+                       x_div=float(K + 1) if k == 1 else 1.0)
+            h = [y]
         return out
 
 
 class PropagateFunction(torch.autograd.Function):
-    """(user, item, brand) weights -> mean of K propagated layers; backward by the same kernel."""
+    """(user, item, brand) weights -> the (user, item, brand) blocks of the mean of K propagated
+    layers (views of one buffer: no torch.cat / torch.split copies either way); backward by the
+    same kernel, reading the three output gradients in place."""
 
     @staticmethod
     def forward(ctx, graph, K, hub_threshold, *segments):
         ctx.graph, ctx.K, ctx.hub_threshold = graph, K, hub_threshold
         ctx.sizes = [int(t.shape[0]) for t in segments]
         segs = [t.detach() for t in segments]
-        return propagate_forward(graph, segs, K, hub_threshold)
+        out = propagate_forward(graph, segs, K, hub_threshold)
+        return tuple(torch.split(out, ctx.sizes, 0))
 
     @staticmethod
-    def backward(ctx, grad):
-        g = propagate_backward(ctx.graph, grad, ctx.K, ctx.hub_threshold)
-        return (None, None, None) + tuple(torch.split(g, ctx.sizes, 0))
+    def backward(ctx, *grads):
+        d = next((g.shape[1] for g in grads if g is not None), None)
+        if d is None:
+            return (None, None, None) + (None,) * len(grads)
+        gs = [g if g is not None else
+              torch.zeros((sz, d), dtype=torch.float32, device=ctx.graph.device)
+              for g, sz in zip(grads, ctx.sizes)]
+        g0 = propagate_backward(ctx.graph, gs, ctx.K, ctx.hub_threshold)
+        return (None, None, None) + tuple(torch.split(g0, ctx.sizes, 0))
 
 
-def propagate(adj, segments, K, hub_threshold=None):
-    """Autograd-aware engine entry used by models.LightGCN / LightGCN_Fusion on a HIP device."""
+def propagate_blocks(adj, segments, K, hub_threshold=None):
+    """Autograd-aware engine entry used by models.LightGCN / LightGCN_Fusion on a HIP device:
+    returns the final embeddings as one block per input segment (user, item, brand)."""
     graph = graph_from_coo(adj)
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
     return PropagateFunction.apply(graph, K, hub_threshold, *segments)
+
+
+def propagate(adj, segments, K, hub_threshold=None):
+    """Like propagate_blocks, as one [n x d] tensor (a concatenating copy: prefer the blocks)."""
+    return torch.cat(propagate_blocks(adj, segments, K, hub_threshold), 0)

@@ -80,13 +80,6 @@ def build_norm_adj_device(train_user, train_item, U, I, B, ib_item=None, ib_bran
         st = engine._stream(dev)
         r_d = torch.from_numpy(rows).to(dev)
         c_d = torch.from_numpy(cols).to(dev)
-        deg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        engine._check(lib.lgcn_adj_degree(P(r_d), ne, n, P(deg), st), "lgcn_adj_degree")
-        rowsum = deg[:n].cpu().numpy().astype(np.float32)
-        with np.errstate(divide="ignore"):
-            dinv = np.power(rowsum, np.float32(-0.5))
-        dinv[np.isinf(dinv)] = np.float32(0.0)
-        dinv_d = torch.from_numpy(dinv).to(dev)
         m = max(ne, 1)
         keys_a = torch.empty(m, dtype=torch.int64, device=dev)
         keys_b = torch.empty(m, dtype=torch.int64, device=dev)
@@ -101,7 +94,15 @@ def build_norm_adj_device(train_user, train_item, U, I, B, ib_item=None, ib_bran
         engine._check(lib.lgcn_adj_sort_unique(P(r_d), P(c_d), ne, n, P(keys_a), P(keys_b),
                                                P(uniq), P(counts), P(n_unique), P(temp),
                                                ctypes.byref(nbytes), st), "lgcn_adj_sort_unique")
-        del temp, keys_a, keys_b, r_d, c_d
+        del temp, keys_a, r_d, c_d
+        deg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        engine._check(lib.lgcn_adj_degree(P(keys_b), ne, n, P(deg), st), "lgcn_adj_degree")
+        rowsum = deg[:n].cpu().numpy().astype(np.float32)
+        with np.errstate(divide="ignore"):
+            dinv = np.power(rowsum, np.float32(-0.5))
+        dinv[np.isinf(dinv)] = np.float32(0.0)
+        dinv_d = torch.from_numpy(dinv).to(dev)
+        del keys_b
         nnz = int(n_unique.item())
         idx = torch.empty((2, max(nnz, 1)), dtype=torch.int64, device=dev)
         vals = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)

@@ -54,7 +54,7 @@ extern "C" {
 /* epilogue modes of lgcn_spmm_layer / lgcn_hub_combine */
 #define LGCN_EPI_STORE 0  /* Y = Â·X */
 #define LGCN_EPI_MEAN  1  /* Y = (((P0 + P1) + ... + P_{n-1}) + Â·X) / div   (lightgcn.py:54) */
-#define LGCN_EPI_ADD   2  /* Y = Z + Â·X                (backward Horner step) */
+#define LGCN_EPI_ADD   2  /* Y = Z / div + Â·X          (backward Horner step) */
 
 typedef int64_t lgcn_edge_t;
 
@@ -86,8 +86,9 @@ typedef struct {
     int32_t pad;
 } lgcn_hub_row_t;
 
-/* Epilogue operands. prev[0] is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
- * dense layer buffers E1..E_{n_prev-1} with leading dimension ld_prev. */
+/* Epilogue operands. MEAN: prev0 is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
+ * dense layer buffers E1..E_{n_prev-1} with leading dimension ld_prev, div = K+1. ADD: addend
+ * is a segmented block Z, div its divisor (1 = plain add; the backward passes G and K+1). */
 typedef struct {
     int32_t mode;
     int32_t n_prev;
@@ -96,8 +97,7 @@ typedef struct {
     lgcn_rows_t prev0;
     const float* prev_dense[LGCN_MAX_LAYERS];
     int64_t ld_prev;
-    const float* addend;
-    int64_t ld_add;
+    lgcn_rows_t addend;
 } lgcn_epilogue_t;
 
 /* ---- identification ---------------------------------------------------------------------- */
@@ -143,8 +143,9 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
 
 /* ---- adjacency builder (main.py:313-336 on the device) -------------------------------------- */
 /* deg[r] = number of stored edges with row r (duplicates counted, main.py:326 rowsum of the
- * ones matrix); zeroes deg itself. */
-int lgcn_adj_degree(const int64_t* rows, int64_t n_edges, int32_t n, int32_t* deg, void* stream);
+ * ones matrix), by binary search over the SORTED keys (keys_b of lgcn_adj_sort_unique). */
+int lgcn_adj_degree(const uint64_t* keys_sorted, int64_t n_edges, int32_t n, int32_t* deg,
+                    void* stream);
 
 /* Sort keys row*n+col (64-bit radix) and run-length encode them: uniq[0..*n_unique) ascending
  * (= (row, col) order), counts = duplicate multiplicity m. Two-call protocol for temp (temp ==
@@ -164,14 +165,16 @@ int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, in
 
 /* ---- the propagation (models/lightgcn.py:44-54) -------------------------------------------- */
 
-/* One layer Y = epilogue(Â·X) over rows [0, n_rows):
+/* One layer Y = epilogue(Â·(X / x_div)) over rows [0, n_rows):
  *  - rows with degree <= hub_threshold: one pass, sequential fmaf, epilogue applied in-kernel;
  *  - hub chunks (n_hub_items, from the host planner) write partials[slot*d ...];
  *    lgcn_hub_combine then finishes those rows. Both kinds run in ONE launch.
- * X is read through `x` (segments allowed). Y is [n_rows x ldy]. d in [1, 2048]. */
+ * X is read through `x` (segments allowed); x_div = 1 reads it as is, otherwise every gathered
+ * element is divided by x_div once (ADD epilogue only: the backward's G/(K+1)).
+ * Y is [n_rows x ldy]. d in [1, 2048]. */
 int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
                     int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
-                    float* partials, lgcn_rows_t x, float* y, int64_t ldy, int32_t d,
+                    float* partials, lgcn_rows_t x, float x_div, float* y, int64_t ldy, int32_t d,
                     const lgcn_epilogue_t* epi_host, void* stream);
 
 /* Finish hub rows: sum each row's partial slots in slot order, apply the epilogue, write Y. */
@@ -195,14 +198,14 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int3
                            void* const* ev_host, void* stream);
 
 /* Whole backward: grad_e0 = sum_k (Âᵀ)^k G/(K+1) in the Horner order autograd uses
- * (h = G/(K+1); K times h = G/(K+1) + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric).
- * work_c, work_h: [n x d] scratch. grad_out/grad_e0 are [n x d] with ld = d. */
+ * (c = G/(K+1); h = c; K times h = c + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric).
+ * G is read in place as segments (the user/item/brand output grads); c is never stored.
+ * work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. */
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, float* partials, const float* grad_out,
-                            int32_t d, int32_t K, float* work_c, float* work_h, float* grad_e0,
-                            void* stream);
+                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out, int32_t d,
+                            int32_t K, float* work_h, float* grad_e0, void* stream);
 
 /* ---- evaluation (main.py:404-439) ----------------------------------------------------------- */
 /* Item splits for lgcn_score_topk: ~2 blocks per CU, >= 2048 items per split, <= 256. */

@@ -46,8 +46,9 @@ class LightGCN(nn.Module):
 
     # -- propagation ------------------------------------------------------------------------
     def _propagate(self, adj_mat, segments):
+        """(final_user, final_item, final_brand) blocks."""
         if adj_mat.device.type == "cuda":
-            final = engine.propagate(adj_mat, segments, self.n_layers)
+            final = engine.propagate_blocks(adj_mat, segments, self.n_layers)
             if self.debug:
                 with torch.no_grad():
                     _, layers = engine.propagate_forward(
@@ -68,7 +69,8 @@ class LightGCN(nn.Module):
             if self.debug:
                 brand_emb_i = ego[self.num_users + self.num_items:]
                 print(f"Layer {i + 1} brand embedding L2 norm: {brand_emb_i.norm(2).item():.6f}")
-        return torch.mean(torch.stack(all_embeddings, dim=0), dim=0)
+        final = torch.mean(torch.stack(all_embeddings, dim=0), dim=0)
+        return torch.split(final, [self.num_users, self.num_items, self.num_brands])
 
     def _last_layer(self, adj_mat, layers, segments):
         g = engine.graph_from_coo(adj_mat)
@@ -82,9 +84,8 @@ class LightGCN(nn.Module):
         user_emb_0 = self.user_embedding.weight
         item_emb_0 = self.item_embedding.weight
         brand_emb_0 = self.brand_embedding.weight
-        final_embeddings = self._propagate(adj_mat, [user_emb_0, item_emb_0, brand_emb_0])
-        final_user_emb, final_item_emb, final_brand_emb = torch.split(
-            final_embeddings, [self.num_users, self.num_items, self.num_brands])
+        final_user_emb, final_item_emb, final_brand_emb = self._propagate(
+            adj_mat, [user_emb_0, item_emb_0, brand_emb_0])
         if self.debug:
             self._debug_cosine(adj_mat, final_item_emb, user_emb_0, item_emb_0)
         return final_user_emb, final_item_emb, final_brand_emb, user_emb_0, item_emb_0

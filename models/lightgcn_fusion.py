@@ -47,7 +47,8 @@ class LightGCN_Fusion(nn.Module):
         fused_item_emb_0 = self.fused_item_embedding()
         segments = [user_emb_0, fused_item_emb_0, brand_emb_0]
         if adj_mat.device.type == "cuda":
-            final_embeddings = engine.propagate(adj_mat, segments, self.n_layers)
+            final_user_emb, final_item_emb, final_brand_emb = engine.propagate_blocks(
+                adj_mat, segments, self.n_layers)
         else:  # CPU adjacency: the reference's ATen path (lightgcn_fusion.py:52-59)
             ego = torch.cat(segments, dim=0)
             all_embeddings = [ego]
@@ -55,8 +56,8 @@ class LightGCN_Fusion(nn.Module):
                 ego = torch.sparse.mm(adj_mat, ego)
                 all_embeddings.append(ego)
             final_embeddings = torch.mean(torch.stack(all_embeddings, dim=0), dim=0)
-        final_user_emb, final_item_emb, final_brand_emb = torch.split(
-            final_embeddings, [self.num_users, self.num_items, self.num_brands])
+            final_user_emb, final_item_emb, final_brand_emb = torch.split(
+                final_embeddings, [self.num_users, self.num_items, self.num_brands])
         return final_user_emb, final_item_emb, final_brand_emb, user_emb_0, item_id_emb_0
 
     def set_graph(self, adj_mat):

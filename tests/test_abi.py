@@ -53,12 +53,14 @@ def test_argument_validation_without_gpu(lib):
     ep.mode = 7
     rows = engine.RowsT()
     # bad epilogue / bad d / negative sizes return before any HIP call
-    assert lib.lgcn_spmm_layer(None, None, 0, 0, None, 0, None, rows, None, 0, 64,
+    assert lib.lgcn_spmm_layer(None, None, 0, 0, None, 0, None, rows, 1.0, None, 0, 64,
                                ctypes.byref(ep), None) == -1
     ep.mode = engine.LGCN_EPI_STORE
-    assert lib.lgcn_spmm_layer(None, None, 10, 0, None, 0, None, rows, None, 0, 0,
+    assert lib.lgcn_spmm_layer(None, None, 10, 0, None, 0, None, rows, 1.0, None, 0, 0,
                                ctypes.byref(ep), None) == -1
-    assert lib.lgcn_spmm_layer(None, None, -1, 0, None, 0, None, rows, None, 0, 64,
+    assert lib.lgcn_spmm_layer(None, None, -1, 0, None, 0, None, rows, 1.0, None, 0, 64,
+                               ctypes.byref(ep), None) == -1
+    assert lib.lgcn_spmm_layer(None, None, 0, 0, None, 0, None, rows, 0.0, None, 64, 64,
                                ctypes.byref(ep), None) == -1
     ep.mode = engine.LGCN_EPI_MEAN
     ep.n_prev = 18
@@ -80,9 +82,9 @@ def test_struct_layout_matches_header():
 int main(void){
  printf("%zu %zu %zu %zu\n", sizeof(lgcn_rows_t), sizeof(lgcn_epilogue_t),
         sizeof(lgcn_hub_item_t), sizeof(lgcn_hub_row_t));
- printf("%zu %zu %zu %zu %zu\n", offsetof(lgcn_epilogue_t, prev0),
+ printf("%zu %zu %zu %zu\n", offsetof(lgcn_epilogue_t, prev0),
         offsetof(lgcn_epilogue_t, prev_dense), offsetof(lgcn_epilogue_t, ld_prev),
-        offsetof(lgcn_epilogue_t, addend), offsetof(lgcn_epilogue_t, ld_add));
+        offsetof(lgcn_epilogue_t, addend));
  return 0;}
 """
     with tempfile.TemporaryDirectory() as td:
@@ -95,8 +97,7 @@ int main(void){
     offs = [int(x) for x in l2.split()]
     assert sizes == [ctypes.sizeof(engine.RowsT), ctypes.sizeof(engine.EpilogueT), 16, 16]
     E = engine.EpilogueT
-    assert offs == [E.prev0.offset, E.prev_dense.offset, E.ld_prev.offset, E.addend.offset,
-                    E.ld_add.offset]
+    assert offs == [E.prev0.offset, E.prev_dense.offset, E.ld_prev.offset, E.addend.offset]
 
 
 def test_engine_refuses_missing_library(tmp_path):
