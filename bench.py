@@ -323,6 +323,23 @@ def main():
         "adjacency_build": builder,
     }
 
+    # backward propagation alone (the K engine layers autograd runs per training batch)
+    gsegs = [out[:U].clone(), out[U:].clone()]
+    for _ in range(2):
+        engine.propagate_backward(g, gsegs, K, hub_thr)
+    torch.cuda.synchronize()
+    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(args.steps):
+        engine.propagate_backward(g, gsegs, K, hub_thr)
+    e.record()
+    torch.cuda.synchronize()
+    bwd_ms = a.elapsed_time(e) / args.steps
+    result["backward"] = {"ms_per_step": round(bwd_ms, 4),
+                          "propagated_edges_per_s": round(K * nnz / (bwd_ms / 1e3), 1),
+                          "what": "dE0 = sum_k (Â^T)^k G/(K+1), Horner order, G read in place"}
+    del gsegs
+
     if not fusion:
         result["eval_topk"] = bench_eval(out, U, I, r, c, dev, args)
 

@@ -71,14 +71,33 @@ __device__ __forceinline__ int2 load_edge(const lgcn_edge_t* e) {
 
 // Sequential fmaf chain over edge records [beg, end) — the ATen CPU order (one row's nonzeros in
 // stored order, y = fma(val, x, y) starting from +0). U gathers are in flight before the folds.
-template <typename V, bool XD>
+// x / div, correctly rounded. When div is a power of two, x * (1/div) is the same real number,
+// so it rounds identically and costs one multiply instead of the IEEE division sequence.
+template <typename V>
+__device__ __forceinline__ V div_exact(V v, float div, bool pow2) {
+    if (pow2) {
+        const float inv = 1.0f / div;
+        if constexpr (VT<V>::W == 4) return make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
+        else return v * inv;
+    }
+    return VT<V>::div(v, div);
+}
+
+__host__ __device__ __forceinline__ bool is_pow2f(float x) {
+    int e;
+    return x > 0.f && frexpf(x, &e) == 0.5f;
+}
+
+// XD: 0 = gather X as is, 1 = X / xdiv (IEEE division), 2 = X * (1/xdiv) with xdiv a power of 2
+template <typename V, int XD>
 __device__ __forceinline__ V load_x(const float* p, float xdiv) {
     const V v = VT<V>::load(p);
-    if constexpr (XD) return VT<V>::div(v, xdiv);  // gathered operand = X / xdiv, rounded once
+    if constexpr (XD == 1) return VT<V>::div(v, xdiv);  // gathered operand = X / xdiv, rounded once
+    else if constexpr (XD == 2) return div_exact<V>(v, xdiv, true);
     else return v;
 }
 
-template <typename V, int G, int NV, int U, bool XD = false>
+template <typename V, int G, int NV, int U, int XD = 0>
 __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges, int32_t beg,
                                            int32_t end, const lgcn_rows_t& x, int lane, int dW,
                                            V (&acc)[NV], float xdiv = 1.f) {
@@ -127,10 +146,11 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
             for (int i = 0; i + 1 < ep.n_prev; ++i)
                 s = T::add(s, T::load(ep.prev_dense[i] + (int64_t)row * ep.ld_prev + c * T::W));
             s = T::add(s, out);
-            out = T::div(s, ep.div);
+            out = div_exact<V>(s, ep.div, ep.pad != 0);
         } else if constexpr (MODE == LGCN_EPI_ADD) {
             // Horner step: (Z / div) + Â·X, Z read in place (segments), Z / div rounded once
-            out = T::add(T::div(T::load(seg_row(ep.addend, row) + c * T::W), ep.div), out);
+            out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div,
+                                      ep.pad != 0), out);
         }
         T::store(yr + c * T::W, out);
     }
@@ -144,7 +164,7 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
 //    record wb+l) with the next window prefetched, and reach every lane by shuffles — the only
 //    memory latency left on the critical path is the gather itself;
 //  * U gathers are in flight per group across row boundaries.
-template <typename V, int G, int NV, int MODE, int RPG, int U, bool XD>
+template <typename V, int G, int NV, int MODE, int RPG, int U, int XD>
 __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                                             const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
                                             int32_t hub_thr, int32_t r0, const lgcn_rows_t& x,
@@ -254,7 +274,7 @@ __device__ __forceinline__ void mean_prefetch(const lgcn_epilogue_t& ep, int32_t
     }
 }
 
-template <typename V, int G, int NV, int MODE, int RPG, int U, int NP = 0, bool XD = false>
+template <typename V, int G, int NV, int MODE, int RPG, int U, int NP = 0, int XD = 0>
 __global__ __launch_bounds__(kBlock) void k_layer(
     const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
     int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
@@ -304,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
                 V s = pre[0][q];
 #pragma unroll
                 for (int p = 1; p < NP; ++p) s = T::add(s, pre[p][q]);
-                T::store(yr + c * T::W, T::div(T::add(s, acc[q]), ep.div));
+                T::store(yr + c * T::W, div_exact<V>(T::add(s, acc[q]), ep.div, ep.pad != 0));
             }
         } else {
             accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv);
@@ -583,8 +603,13 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_
                                hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         case LGCN_EPI_ADD:
-            if (xdiv != 1.f)
-                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, true>),
+            if (xdiv != 1.f && is_pow2f(xdiv))
+                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 2>),
+                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
+                                   thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
+                                   xdiv);
+            else if (xdiv != 1.f)
+                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 1>),
                                    dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
                                    thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
                                    xdiv);
@@ -732,10 +757,17 @@ struct ScaleF {
     }
 };
 
+lgcn_epilogue_t with_pow2(const lgcn_epilogue_t& ep) {
+    lgcn_epilogue_t e = ep;
+    e.pad = is_pow2f(ep.div) ? 1 : 0;  // internal: divisions by div may multiply by 1/div
+    return e;
+}
+
 int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
                const lgcn_hub_item_t* items, int32_t n_items, float* partials, lgcn_rows_t x,
-               float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, float xdiv,
+               float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep_in, float xdiv,
                hipStream_t s) {
+    const lgcn_epilogue_t ep = with_pow2(ep_in);
     const bool vec_ok = rows_aligned(x) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep) &&
                         (n_items == 0 || al16(partials));
     const Geo g = pick_geo(d, vec_ok);
@@ -745,8 +777,9 @@ int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, 
 }
 
 int hub_combine(const lgcn_hub_row_t* rows, int32_t n, const float* partials, float* y,
-                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep_in, hipStream_t s) {
     if (n <= 0) return 0;
+    const lgcn_epilogue_t ep = with_pow2(ep_in);
     const bool vec_ok = al16(partials) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep);
     const Geo g = pick_geo(d, vec_ok);
     CombineF f{rows, n, partials, y, ldy, d, g.dW, &ep, s};

@@ -93,7 +93,7 @@ typedef struct {
     int32_t mode;
     int32_t n_prev;
     float div;
-    int32_t pad;
+    int32_t pad;          /* reserved: the engine overwrites it */
     lgcn_rows_t prev0;
     const float* prev_dense[LGCN_MAX_LAYERS];
     int64_t ld_prev;
