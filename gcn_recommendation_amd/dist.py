@@ -32,13 +32,13 @@ from . import engine
 # ----------------------------------------------------------------------------------------------
 # process group
 # ----------------------------------------------------------------------------------------------
-def init(device_type="cuda"):
+def init(device_type="cuda", backend=None):
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    backend = "nccl" if device_type == "cuda" else "gloo"
+    backend = backend or ("nccl" if device_type == "cuda" else "gloo")
     kw = {}
-    if device_type == "cuda":
+    if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     dist.init_process_group(backend=backend, **kw)
     return dist.get_rank(), dist.get_world_size()
@@ -113,6 +113,17 @@ class RowPartPlan:
         return (self.world - 1) * self.n_max * d * 4
 
 
+def allgather_into(out, inp):
+    """all_gather_into_tensor; with the gloo backend and HIP tensors (the 2-process GPU test on a
+    one-GPU box) the exchange bounces through host memory."""
+    if out.device.type == "cuda" and dist.get_backend() == "gloo":
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu())
+        out.copy_(o)
+        return
+    dist.all_gather_into_tensor(out, inp)
+
+
 def _local_layer(graph, xs, y, d, ep, hub_thr):
     """y[:n_local] = epilogue(Â_local · X): engine on HIP, the reference ATen op on CPU."""
     if y.device.type == "cuda":
@@ -175,11 +186,11 @@ def rowpart_forward(plan, segments, K, hub_thr=None, gather_final=True, layer_ev
         if layer_events is not None:
             layer_events[k - 1][1].record()
         if k < K:  # in-place all-gather: this rank's chunk is already in place
-            dist.all_gather_into_tensor(bufs[k - 1], bufs[k - 1][rk * nm:(rk + 1) * nm])
+            allgather_into(bufs[k - 1], bufs[k - 1][rk * nm:(rk + 1) * nm])
     if not gather_final:
         return out_local[:nl]
     full = torch.empty((W * nm, d), dtype=torch.float32, device=dev)
-    dist.all_gather_into_tensor(full, out_local)
+    allgather_into(full, out_local)
     return full
 
 
