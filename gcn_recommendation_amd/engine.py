@@ -365,7 +365,9 @@ def _check_emb(segments, d, device):
             raise LgcnError(f"embedding on {t.device}, adjacency on {device}")
         if t.dtype != torch.float32:
             raise LgcnError("embeddings must be float32")
-        if t.dim() != 2 or t.shape[1] != d or t.stride(1) != 1 or t.stride(0) != d:
+        if t.dim() != 2 or t.shape[1] != d:
+            raise LgcnError("embedding blocks must be [rows x d]")
+        if t.shape[0] > 0 and (t.stride(1) != 1 or t.stride(0) != d):
             raise LgcnError("embedding blocks must be contiguous [rows x d]")
 
 
