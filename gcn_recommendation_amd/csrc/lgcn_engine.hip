@@ -74,12 +74,15 @@ __device__ __forceinline__ int2 load_edge(const lgcn_edge_t* e) {
 // x / div, correctly rounded. When div is a power of two, x * (1/div) is the same real number,
 // so it rounds identically and costs one multiply instead of the IEEE division sequence.
 template <typename V>
-__device__ __forceinline__ V div_exact(V v, float div, bool pow2) {
-    if (pow2) {
-        const float inv = 1.0f / div;
-        if constexpr (VT<V>::W == 4) return make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
-        else return v * inv;
-    }
+__device__ __forceinline__ V mul_s(V v, float s) {
+    if constexpr (VT<V>::W == 4) return make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
+    else return v * s;
+}
+
+// inv_bits: 0, or the bits of 1/div when div is a power of two (precomputed on the host)
+template <typename V>
+__device__ __forceinline__ V div_exact(V v, float div, int32_t inv_bits) {
+    if (inv_bits != 0) return mul_s<V>(v, __int_as_float(inv_bits));
     return VT<V>::div(v, div);
 }
 
@@ -88,12 +91,13 @@ __host__ __device__ __forceinline__ bool is_pow2f(float x) {
     return x > 0.f && frexpf(x, &e) == 0.5f;
 }
 
-// XD: 0 = gather X as is, 1 = X / xdiv (IEEE division), 2 = X * (1/xdiv) with xdiv a power of 2
+// XD: 0 = gather X as is, 1 = X / xdiv (IEEE division), 2 = X * xdiv where the host already
+// replaced a power-of-two divisor by its (exact) reciprocal
 template <typename V, int XD>
 __device__ __forceinline__ V load_x(const float* p, float xdiv) {
     const V v = VT<V>::load(p);
     if constexpr (XD == 1) return VT<V>::div(v, xdiv);  // gathered operand = X / xdiv, rounded once
-    else if constexpr (XD == 2) return div_exact<V>(v, xdiv, true);
+    else if constexpr (XD == 2) return mul_s<V>(v, xdiv);  // host passes 1/xdiv (exact)
     else return v;
 }
 
@@ -146,11 +150,10 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
             for (int i = 0; i + 1 < ep.n_prev; ++i)
                 s = T::add(s, T::load(ep.prev_dense[i] + (int64_t)row * ep.ld_prev + c * T::W));
             s = T::add(s, out);
-            out = div_exact<V>(s, ep.div, ep.pad != 0);
+            out = div_exact<V>(s, ep.div, ep.pad);
         } else if constexpr (MODE == LGCN_EPI_ADD) {
             // Horner step: (Z / div) + Â·X, Z read in place (segments), Z / div rounded once
-            out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div,
-                                      ep.pad != 0), out);
+            out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div, ep.pad), out);
         }
         T::store(yr + c * T::W, out);
     }
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
                 V s = pre[0][q];
 #pragma unroll
                 for (int p = 1; p < NP; ++p) s = T::add(s, pre[p][q]);
-                T::store(yr + c * T::W, div_exact<V>(T::add(s, acc[q]), ep.div, ep.pad != 0));
+                T::store(yr + c * T::W, div_exact<V>(T::add(s, acc[q]), ep.div, ep.pad));
             }
         } else {
             accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv);
@@ -607,7 +610,7 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_
                 hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 2>),
                                    dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
                                    thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
-                                   xdiv);
+                                   1.0f / xdiv);
             else if (xdiv != 1.f)
                 hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 1>),
                                    dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
@@ -651,7 +654,20 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_ro
         return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
     }
     if (RB <= 1 || g_rows_per_group == 1) return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
-    return launch_layer_rpg<V, G, NV, RB, UB>(LGCN_ARGS);
+    // keep >= ~64k lane groups in the grid: small graphs (the reference's real datasets) run
+    // one row per group, Books-scale graphs 15-row bundles
+    const int64_t per = (int64_t)n_rows / 65536;
+    if (per >= RB) return launch_layer_rpg<V, G, NV, RB, UB>(LGCN_ARGS);
+    if constexpr (RB >= 8) {
+        if (per >= 8) return launch_layer_rpg<V, G, NV, 8, UB>(LGCN_ARGS);
+    }
+    if constexpr (RB >= 4) {
+        if (per >= 4) return launch_layer_rpg<V, G, NV, 4, UB>(LGCN_ARGS);
+    }
+    if constexpr (RB >= 2) {
+        if (per >= 2) return launch_layer_rpg<V, G, NV, 2, UB>(LGCN_ARGS);
+    }
+    return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
 #undef LGCN_ARGS
 }
 
@@ -759,7 +775,13 @@ struct ScaleF {
 
 lgcn_epilogue_t with_pow2(const lgcn_epilogue_t& ep) {
     lgcn_epilogue_t e = ep;
-    e.pad = is_pow2f(ep.div) ? 1 : 0;  // internal: divisions by div may multiply by 1/div
+    // internal: divisions by a power-of-two div become multiplies by its exact reciprocal
+    if (is_pow2f(ep.div)) {
+        const float inv = 1.0f / ep.div;
+        memcpy(&e.pad, &inv, sizeof(inv));
+    } else {
+        e.pad = 0;
+    }
     return e;
 }
 
