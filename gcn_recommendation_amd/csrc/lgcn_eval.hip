@@ -52,6 +52,8 @@ struct WaveState {
     int32_t idx[kUsersPerWave][kCap];
     int32_t cnt[kUsersPerWave];
     float thr[kUsersPerWave];
+    int32_t mlo[kUsersPerWave];  // the user's train items: mask_items[mlo, mhi); mhi < mlo: no user
+    int32_t mhi[kUsersPerWave];
 };
 
 // Keep the K best of user u's buffer (entries at ranks >= K dropped), set its threshold.
@@ -117,46 +119,58 @@ __global__ __launch_bounds__(kWaves * 64) void k_score_topk(
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
         }
     }
-    // rows of the C/D tile this lane holds: user (ub + row(r)), row(r) = (r&3)+8(r>>2)+4h
-    int32_t mlo[16], mhi[16];
-    float thr[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool ok = ub + row < n_users;
-        const int32_t u = ok ? users[ub + row] : 0;
-        mlo[r] = ok ? mrow[u] : 0;
-        mhi[r] = ok ? mrow[u + 1] : -1;  // hi < lo marks an invalid user slot
-        thr[r] = -INFINITY;
+    if (lane < kUsersPerWave) {
+        const bool ok = ub + lane < n_users;
+        const int32_t u = ok ? users[ub + lane] : 0;
+        st.mlo[lane] = ok ? mrow[u] : 0;
+        st.mhi[lane] = ok ? mrow[u + 1] : -1;
     }
     __builtin_amdgcn_wave_barrier();
-
-    for (int32_t t0 = it0; t0 < it1; t0 += 32) {
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_wave_barrier();
+    // rows of the C/D tile this lane holds: user (ub + row(r)), row(r) = (r&3)+8(r>>2)+4h.
+    // The B operand (32 items x this lane's feature half) is double-buffered: the next tile's
+    // loads are in flight during the current tile's MFMA chain.
+    float4 bcur[DH / 4], bnxt[DH / 4];
+    auto load_tile = [&](int32_t t0, float4 (&b)[DH / 4]) {
         const int32_t item = t0 + col;
         const bool iok = item < it1;
         const float* ir = iemb + (iok ? (int64_t)item * ld_i : 0) + h * DH;
+#pragma unroll
+        for (int q = 0; q < DH / 4; ++q)
+            b[q] = iok ? *reinterpret_cast<const float4*>(ir + 4 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    if (it0 < it1) load_tile(it0, bcur);
+
+    for (int32_t t0 = it0; t0 < it1; t0 += 32) {
+        if (t0 + 32 < it1) load_tile(t0 + 32, bnxt);
+        const int32_t item = t0 + col;
+        const bool iok = item < it1;
         f32x16 acc = {};
 #pragma unroll
         for (int q = 0; q < DH / 4; ++q) {
-            const float4 v = iok ? *reinterpret_cast<const float4*>(ir + 4 * q)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q], v.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q + 1], v.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q + 2], v.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q + 3], v.w, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q], bcur[q].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q + 1], bcur[q].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q + 2], bcur[q].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * q + 3], bcur[q].w, acc, 0, 0, 0);
         }
         bool any = false;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
             float sc = acc[r];
-            if (iok && mhi[r] >= mlo[r] && sc > thr[r]) {
-                if (in_sorted(mitems, mlo[r], mhi[r], item)) sc = kMasked;  // main.py:422-424
-                if (sc > thr[r]) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int pos = atomicAdd(&st.cnt[row], 1);
-                    st.score[row][pos] = sc;
-                    st.idx[row][pos] = item;
-                    any = true;
+            const float thr = st.thr[row];
+            if (iok && sc > thr) {
+                const int32_t lo = st.mlo[row], hi = st.mhi[row];
+                if (hi >= lo) {
+                    if (in_sorted(mitems, lo, hi, item)) sc = kMasked;  // main.py:422-424
+                    if (sc > thr) {
+                        const int pos = atomicAdd(&st.cnt[row], 1);
+                        st.score[row][pos] = sc;
+                        st.idx[row][pos] = item;
+                        any = true;
+                    }
                 }
             }
         }
@@ -171,9 +185,9 @@ __global__ __launch_bounds__(kWaves * 64) void k_score_topk(
                 need &= need - 1;
                 compact_user(st, u, K, lane);
             }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) thr[r] = st.thr[(r & 3) + 8 * (r >> 2) + 4 * h];
         }
+#pragma unroll
+        for (int q = 0; q < DH / 4; ++q) bcur[q] = bnxt[q];
     }
     // final: every buffer to its K best in rank order, written to this split's partial list
     for (int u = 0; u < kUsersPerWave; ++u) {
