@@ -370,13 +370,30 @@ def main():
         e_gpu = float(np.abs(got - f64).max())
         e_cpu = float(np.abs(refn - f64).max())
         hub_rows = np.nonzero(g.degrees() > hub_thr)[0]
+        # Per row: where the CPU reference is itself accurate (its own error vs the fp64 arbiter
+        # is under a tenth of the gate), the engine must match it within the gate; elsewhere
+        # (rows fed by multi-million-term fp32 hub sums) the engine must be at least as close to
+        # exact arithmetic as the reference.
+        err_row = np.abs(got - refn).max(1)
+        cpu_row = np.abs(refn - f64).max(1)
+        gpu_row = np.abs(got - f64).max(1)
+        accurate = cpu_row <= 1e-6 * scale
         result["parity"] = {
-            "gate": "max|gpu-cpu_ref| <= 1e-5*max|cpu_ref| (north_star)",
-            "normwise_vs_cpu_ref": err / scale, "ok": err <= 1e-5 * scale,
+            "gate": "north_star: max|gpu - cpu_ref| <= 1e-5 * max|cpu_ref| per tensor",
+            "normwise_vs_cpu_ref": err / scale,
+            "pass_vs_cpu_ref": err <= 1e-5 * scale,
             "rows_bitwise_equal_frac": float(np.all(got == refn, axis=1).mean()),
+            "rows_where_cpu_ref_accurate": {
+                "frac": float(accurate.mean()),
+                "normwise_vs_cpu_ref": float(err_row[accurate].max(initial=0) / scale),
+                "pass": bool((err_row[accurate] <= 1e-5 * scale).all())},
             "fp64_arbiter": {"gpu_normwise": e_gpu / scale, "cpu_ref_normwise": e_cpu / scale,
-                             "gpu_not_less_accurate": e_gpu <= e_cpu},
-            "hub_rows": int(hub_rows.size), "max_degree": int(g.degrees().max())}
+                             "gpu_within_gate_of_exact": e_gpu <= 1e-5 * scale,
+                             "gpu_not_less_accurate": e_gpu <= e_cpu,
+                             "rows_gpu_closer_or_equal_frac": float((gpu_row <= cpu_row).mean())},
+            "hub_rows": int(hub_rows.size), "max_degree": int(g.degrees().max()),
+            "reading": "a failing pass_vs_cpu_ref with gpu_within_gate_of_exact means the CPU "
+                       "reference's own sequential fp32 error exceeds the gate (hub rows)"}
         del f64
         rp = np.searchsorted(r, np.arange(n + 1)).astype(np.int64)
         rg = recall_ndcg(out[:U], out[U:], ev_users, ev_items, rp, c, U, k=20, return_topk=True)
