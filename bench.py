@@ -403,6 +403,8 @@ def main():
                               "identical": rg[:2] == rc[:2], "users": int(len(ev_users)),
                               "top20_lists_identical_frac": float(
                                   np.all(rg[2] == rc[2], axis=1).mean()),
+                              "top20_sets_identical_frac": float(np.mean(
+                                  [set(a) == set(b) for a, b in zip(rg[2], rc[2])])),
                               "note": "random-init embeddings and random held-out items: recall "
                                       "is ~0 by construction; the top-20 list agreement is the "
                                       "informative parity number"}
