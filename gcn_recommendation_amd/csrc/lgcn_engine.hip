@@ -169,7 +169,8 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
 //  * U gathers are in flight per group across row boundaries.
 template <typename V, int G, int NV, int MODE, int RPG, int U, int XD>
 __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
-                                            const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
+                                            const lgcn_edge_t* __restrict__ edges,
+                                            const int32_t* __restrict__ row_ids, int32_t n_rows,
                                             int32_t hub_thr, int32_t r0, const lgcn_rows_t& x,
                                             float* __restrict__ y, int64_t ldy, int lane, int dW,
                                             const lgcn_epilogue_t& ep, float xdiv) {
@@ -179,6 +180,9 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     // lane l (l <= nrows) holds rowptr[r0 + l]; boundaries are read back by shuffles
     const int32_t rpl = (lane <= nrows) ? rowptr[r0 + lane] : 0;
     auto bnd = [&](int i) { return __shfl(rpl, i, G); };
+    // lane l (l < nrows) holds the output row of slot r0 + l (the CSR may be stored in a
+    // processing order: slot s holds the edges of row row_ids[s])
+    const int32_t orl = (lane < nrows) ? (row_ids ? row_ids[r0 + lane] : r0 + lane) : 0;
     const int32_t eend = bnd(nrows);
     auto load_win = [&](int32_t b) {
         return (b + lane < eend) ? load_edge(edges + b + lane) : make_int2(0, 0);
@@ -196,7 +200,8 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     int2 nxt = load_win(wb + G);
     auto flush = [&](int i) {
         const int32_t deg = bnd(i + 1) - bnd(i);
-        if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, r0 + i, lane, dW, acc, y, ldy);
+        const int32_t orow = __shfl(orl, i, G);
+        if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, orow, lane, dW, acc, y, ldy);
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
     };
@@ -279,7 +284,8 @@ __device__ __forceinline__ void mean_prefetch(const lgcn_epilogue_t& ep, int32_t
 
 template <typename V, int G, int NV, int MODE, int RPG, int U, int NP = 0, int XD = 0>
 __global__ __launch_bounds__(kBlock) void k_layer(
-    const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges, int32_t n_rows,
+    const int32_t* __restrict__ rowptr, const lgcn_edge_t* __restrict__ edges,
+    const int32_t* __restrict__ row_ids, int32_t n_rows,
     int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
     int32_t hub_blocks, float* __restrict__ partials, lgcn_rows_t x, float* __restrict__ y,
     int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep, float xdiv) {
@@ -307,11 +313,12 @@ __global__ __launch_bounds__(kBlock) void k_layer(
     }
     const int64_t gidx = (int64_t)(blockIdx.x - hub_blocks) * RPB + grp;
     if constexpr (RPG == 1) {
-        const int32_t row = (int32_t)gidx;
         if (gidx >= n_rows) return;
-        const int32_t beg = rowptr[row];
-        const int32_t end = rowptr[row + 1];
+        const int32_t slot = (int32_t)gidx;
+        const int32_t beg = rowptr[slot];
+        const int32_t end = rowptr[slot + 1];
         if (end - beg > hub_thr) return;  // owned by the hub chunks + k_hub_combine
+        const int32_t row = row_ids ? row_ids[slot] : slot;  // output row of this slot
         V acc[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
@@ -336,8 +343,8 @@ __global__ __launch_bounds__(kBlock) void k_layer(
     } else {
         const int64_t r0 = gidx * RPG;
         if (r0 >= n_rows) return;
-        rows_bundle<V, G, NV, MODE, RPG, U, XD>(rowptr, edges, n_rows, hub_thr, (int32_t)r0, x, y,
-                                                ldy, lane, dW, ep, xdiv);
+        rows_bundle<V, G, NV, MODE, RPG, U, XD>(rowptr, edges, row_ids, n_rows, hub_thr,
+                                                (int32_t)r0, x, y, ldy, lane, dW, ep, xdiv);
     }
 }
 
@@ -480,6 +487,33 @@ __global__ void k_csr_symmetric(const int32_t* __restrict__ rowptr,
         atomicOr(asym, 1);
 }
 
+// Processing order: slots sorted by degree (descending, stable). The lane groups of a wave then
+// stream rows of equal length (no group idles while a longer neighbour finishes) and hub rows
+// come first. Each row keeps its own edge order, so every output row is the same fp32 chain.
+__global__ void k_csr_degrees(const int32_t* __restrict__ rowptr, int32_t n,
+                              int32_t* __restrict__ deg, int32_t* __restrict__ iota) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    deg[r] = rowptr[r + 1] - rowptr[r];
+    iota[r] = (int32_t)r;
+}
+
+// edges_out[j] = the edge record of slot s (binary search: rowptr_out[s] <= j < rowptr_out[s+1])
+__global__ void k_csr_gather_rows(const int32_t* __restrict__ rowptr_out,
+                                  const int32_t* __restrict__ row_ids,
+                                  const int32_t* __restrict__ rowptr,
+                                  const lgcn_edge_t* __restrict__ edges, int32_t n, int64_t nnz,
+                                  lgcn_edge_t* __restrict__ edges_out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    int32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        if (rowptr_out[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    edges_out[j] = edges[rowptr[row_ids[lo]] + (j - rowptr_out[lo])];
+}
+
 // ---------------------------------------------------------------------------------------------
 // adjacency builder (main.py:313-336 on the device): degree histogram, duplicate merge by a
 // 64-bit radix sort of row*n+col keys + run-length encode, values fp32((d_r * m) * d_c)
@@ -581,7 +615,8 @@ int g_rows_per_group = 0;
 int g_unroll = 0;
 
 template <typename V, int G, int NV, int RPG, int U, int NP = 0>
-int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                     int32_t n_rows, int32_t thr,
                      const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                      const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
                      const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
@@ -596,29 +631,29 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_
         case LGCN_EPI_STORE:
             if (xdiv != 1.f) return LGCN_EINVAL;  // gather scaling exists for the backward only
             hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_STORE, RPG, U>), dim3((uint32_t)grid),
-                               dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                               dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,
                                hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         case LGCN_EPI_MEAN:
             if (xdiv != 1.f) return LGCN_EINVAL;
             hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN, RPG, U, NP>), dim3((uint32_t)grid),
-                               dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                               dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,
                                hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         case LGCN_EPI_ADD:
             if (xdiv != 1.f && is_pow2f(xdiv))
                 hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 2>),
-                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
+                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows,
                                    thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
                                    1.0f / xdiv);
             else if (xdiv != 1.f)
                 hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 1>),
-                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, n_rows,
+                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows,
                                    thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
                                    xdiv);
             else
                 hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U>), dim3((uint32_t)grid),
-                                   dim3(kBlock), 0, s, rowptr, edges, n_rows, thr, items, n_items,
+                                   dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,
                                    hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
             break;
         default:
@@ -628,7 +663,8 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_
 }
 
 template <typename V, int G, int NV>
-int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                   int32_t n_rows, int32_t thr,
                    const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                    const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
                    const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
@@ -637,7 +673,7 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_ro
     constexpr int U1 = NV >= 8 ? 1 : 8 / NV;
     constexpr int UB = NV >= 4 ? 1 : 4 / NV;
     constexpr int RB = G >= 16 ? 15 : G - 1;
-#define LGCN_ARGS rowptr, edges, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, xdiv, s
+#define LGCN_ARGS rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, xdiv, s
     if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: explicit variants (lgcn_tune)
 #define LGCN_V(R_, U_) \
         if (g_rows_per_group == R_ && g_unroll == U_) return launch_layer_rpg<V, G, NV, R_, U_>(LGCN_ARGS);
@@ -749,11 +785,11 @@ int check_epi(const lgcn_epilogue_t* ep) {
 }
 
 struct LayerF {
-    const int32_t* rowptr; const lgcn_edge_t* edges; int32_t n_rows, thr;
+    const int32_t* rowptr; const lgcn_edge_t* edges; const int32_t* row_ids; int32_t n_rows, thr;
     const lgcn_hub_item_t* items; int32_t n_items; float* partials; const lgcn_rows_t* x;
     float* y; int64_t ldy; int32_t d, dW; const lgcn_epilogue_t* ep; float xdiv; hipStream_t s;
     template <typename V, int G, int NV> int operator()() const {
-        return launch_layer_t<V, G, NV>(rowptr, edges, n_rows, thr, items, n_items, partials, *x,
+        return launch_layer_t<V, G, NV>(rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, *x,
                                         y, ldy, d, dW, *ep, xdiv, s);
     }
 };
@@ -785,7 +821,8 @@ lgcn_epilogue_t with_pow2(const lgcn_epilogue_t& ep) {
     return e;
 }
 
-int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, int32_t thr,
+int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+               int32_t n_rows, int32_t thr,
                const lgcn_hub_item_t* items, int32_t n_items, float* partials, lgcn_rows_t x,
                float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep_in, float xdiv,
                hipStream_t s) {
@@ -793,7 +830,7 @@ int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows, 
     const bool vec_ok = rows_aligned(x) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep) &&
                         (n_items == 0 || al16(partials));
     const Geo g = pick_geo(d, vec_ok);
-    LayerF f{rowptr, edges, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW, &ep,
+    LayerF f{rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW, &ep,
              xdiv, s};
     return dispatch_geo(g, f);
 }
@@ -939,6 +976,46 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
     return last_err();
 }
 
+int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
+                             int64_t nnz, int32_t* deg_tmp, int32_t* deg_sorted, int32_t* iota_tmp,
+                             int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
+                             void* temp, size_t* temp_bytes_host, void* stream) {
+    if (n_rows < 0 || nnz < 0 || nnz > 0x7fffffffLL || !temp_bytes_host) return LGCN_EINVAL;
+    int end_bit = 1;  // degrees are <= nnz
+    while (end_bit < 31 && (1LL << end_bit) <= nnz) ++end_bit;
+    hipStream_t s = S(stream);
+    const int n = n_rows;
+    if (temp == nullptr) {
+        size_t b1 = 0, b2 = 0;
+        hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(
+            nullptr, b1, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, end_bit, s);
+        if (e != hipSuccess) return (int)e;
+        e = hipcub::DeviceScan::InclusiveSum(nullptr, b2, deg_sorted, rowptr_out, n, s);
+        *temp_bytes_host = b1 > b2 ? b1 : b2;
+        return herr(e);
+    }
+    if (!rowptr || !rowptr_out || (n > 0 && (!deg_tmp || !deg_sorted || !iota_tmp || !row_ids)))
+        return LGCN_EINVAL;
+    if (nnz > 0 && (!edges || !edges_out)) return LGCN_EINVAL;
+    if (int e = herr(hipMemsetAsync(rowptr_out, 0, sizeof(int32_t), s))) return e;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_csr_degrees, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, rowptr, n, deg_tmp, iota_tmp);
+    if (int e = last_err()) return e;
+    size_t bytes = *temp_bytes_host;
+    // LSD radix sort: stable, so rows of equal degree keep their id order
+    if (int e = herr(hipcub::DeviceRadixSort::SortPairsDescending(
+            temp, bytes, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, end_bit, s)))
+        return e;
+    bytes = *temp_bytes_host;
+    if (int e = herr(hipcub::DeviceScan::InclusiveSum(temp, bytes, deg_sorted, rowptr_out + 1, n, s)))
+        return e;
+    if (nnz == 0) return 0;
+    hipLaunchKernelGGL(k_csr_gather_rows, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, s, rowptr_out, row_ids, rowptr, edges, n, nnz, edges_out);
+    return last_err();
+}
+
 int lgcn_adj_degree(const uint64_t* keys_sorted, int64_t n_edges, int32_t n, int32_t* deg,
                     void* stream) {
     if (n_edges < 0 || n < 0 || (n_edges > 0 && !keys_sorted) || (n > 0 && !deg))
@@ -1000,8 +1077,8 @@ int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, in
     return last_err();
 }
 
-int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
-                    int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
+int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                    int32_t n_rows, int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
                     float* partials, lgcn_rows_t x, float x_div, float* y, int64_t ldy, int32_t d,
                     const lgcn_epilogue_t* epi_host, void* stream) {
     if (int e = valid_geom(n_rows, d)) return e;
@@ -1009,7 +1086,7 @@ int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_r
     if (n_rows > 0 && (!rowptr || !y || ldy < d)) return LGCN_EINVAL;
     if (n_hub_items < 0 || (n_hub_items > 0 && (!hub_items || !partials))) return LGCN_EINVAL;
     if (!(x_div > 0.f)) return LGCN_EINVAL;
-    return spmm_layer(rowptr, edges, n_rows, hub_threshold, hub_items, n_hub_items, partials, x, y,
+    return spmm_layer(rowptr, edges, row_ids, n_rows, hub_threshold, hub_items, n_hub_items, partials, x, y,
                       ldy, d, *epi_host, x_div, S(stream));
 }
 
@@ -1029,7 +1106,8 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
     return scale_rows(x, n_rows, d, div, y, ldy, S(stream));
 }
 
-int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
+                           const int32_t* row_ids, int32_t n,
                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
                            int32_t n_hub_rows, float* partials, lgcn_rows_t emb, int32_t d,
@@ -1060,7 +1138,7 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int3
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1)], s))) return e;
         }
-        if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials, x,
+        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items, partials, x,
                                y, d, d, ep, 1.f, s))
             return e;
         if (ev_host) {
@@ -1071,7 +1149,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int3
     return 0;
 }
 
-int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
+                            const int32_t* row_ids, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
                             int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out, int32_t d,
@@ -1093,7 +1172,7 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int
     float xdiv = div;
     for (int k = 1; k <= K; ++k) {
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
-        if (int e = spmm_layer(rowptr, edges, n, hub_threshold, hub_items, n_hub_items, partials, h,
+        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items, partials, h,
                                y, d, d, ep, xdiv, s))
             return e;
         if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;

@@ -24,6 +24,7 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL = 1, 2
+ABI_VERSION = 2
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
@@ -62,6 +63,8 @@ ABI = [
     ("lgcn_coo_sort_perm", ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P,
                                           ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
+    ("lgcn_csr_order_by_degree", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P,
+                                                ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),  # (sorted keys, ...)
     ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
                                             ctypes.POINTER(ctypes.c_size_t), _P]),
@@ -69,15 +72,15 @@ ABI = [
     ("lgcn_eval_splits", ctypes.c_int, [_I32, _I32, _I32]),
     ("lgcn_score_topk", ctypes.c_int, [_P, _I64, _P, _I32, _P, _I64, _I32, _I32, _P, _P, _I32,
                                        _I32, _P, _P, _P, _P, _P]),
-    ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, RowsT, ctypes.c_float,
+    ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, RowsT, ctypes.c_float,
                                        _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _P, _P, _I64, _I32,
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
-    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, RowsT,
-                                              _I32, _I32, _P, _P, _P, _P]),
-    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P, _I32, _P, RowsT,
-                                               _I32, _I32, _P, _P, _P]),
+    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _P,
+                                              RowsT, _I32, _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _P,
+                                               RowsT, _I32, _I32, _P, _P, _P]),
 ]
 
 
@@ -96,7 +99,7 @@ def load_library(path=None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.lgcn_abi_version() != 1:
+        if lib.lgcn_abi_version() != ABI_VERSION:
             raise LgcnError("liblgcn_engine.so ABI version mismatch")
         _lib = lib
         return lib
@@ -155,7 +158,7 @@ def pack_edges(cols, vals):
     return ((v << np.uint64(32)) | c).view(np.int64)
 
 
-def graph_from_host_csr(rowptr, cols, vals, n_cols, device):
+def graph_from_host_csr(rowptr, cols, vals, n_cols, device, order=None):
     """Device CSR (possibly rectangular: a rank's row block with global columns) from host
     arrays already in the engine's order. Forward-only: no transpose is attached."""
     rowptr = np.ascontiguousarray(rowptr, dtype=np.int32)
@@ -165,7 +168,20 @@ def graph_from_host_csr(rowptr, cols, vals, n_cols, device):
     g = Graph(n_rows, n_cols, torch.from_numpy(rowptr).to(device),
               torch.from_numpy(edges).to(device), nnz, device)
     g._rowptr_host = rowptr
+    if row_order(order) == "degree":
+        with torch.cuda.device(device):
+            g = order_by_degree(load_library(), g, _stream(device))
     return g
+
+
+def row_order(order=None):
+    """Processing order of CSR rows: "degree" (default: slots sorted by degree, descending) or
+    "stored" (row id order). Env LGCN_ROW_ORDER overrides the default. Results are identical
+    either way; only the kernels' load balance changes."""
+    o = (order or os.environ.get("LGCN_ROW_ORDER", "degree")).lower()
+    if o not in ("degree", "stored"):
+        raise LgcnError(f"unknown row order {o!r} (degree | stored)")
+    return o
 
 
 def hub_threshold_from_env(default=DEFAULT_HUB_THRESHOLD):
@@ -189,8 +205,9 @@ class HubPlan:
         self.n_slots = n_slots
 
 
-def plan_hubs(rowptr_host, threshold, chunk, device):
-    """Cut rows with degree > threshold into `chunk`-edge pieces (host planner, numpy)."""
+def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None):
+    """Cut rows with degree > threshold into `chunk`-edge pieces (host planner, numpy).
+    rowptr_host is in storage (slot) order; row_ids_host maps a slot to its output row."""
     deg = np.diff(rowptr_host.astype(np.int64))
     hub = np.nonzero(deg > threshold)[0]
     if threshold >= INT32_MAX or hub.size == 0:
@@ -203,37 +220,82 @@ def plan_hubs(rowptr_host, threshold, chunk, device):
     beg = rowptr_host[row_of].astype(np.int64) + k * chunk
     end = np.minimum(beg + chunk, rowptr_host[row_of + 1])
     # longest rows first so their combine inputs are ready early; items in slot order
-    items = np.stack([row_of, beg, end, np.arange(n_slots)], 1).astype(np.int32)
-    rows = np.stack([hub, first, nch, np.zeros_like(hub)], 1).astype(np.int32)
+    out_row = hub if row_ids_host is None else row_ids_host[hub]
+    items = np.stack([np.repeat(out_row, nch), beg, end, np.arange(n_slots)], 1).astype(np.int32)
+    rows = np.stack([out_row, first, nch, np.zeros_like(hub)], 1).astype(np.int32)
     return HubPlan(threshold, chunk, torch.from_numpy(items).to(device),
                    torch.from_numpy(rows).to(device), n_slots)
 
 
 class Graph:
-    """Device CSR of a square Â plus its backward operator (Âᵀ, == Â when bitwise symmetric)."""
+    """Device CSR of a square Â plus its backward operator (Âᵀ, == Â when bitwise symmetric).
 
-    def __init__(self, n_rows, n_cols, rowptr, edges, nnz, device):
+    rowptr/edges are in storage order: row id order, or — when row_ids is set — degree-ordered
+    slots (slot s holds the edges of row row_ids[s], lgcn_csr_order_by_degree)."""
+
+    def __init__(self, n_rows, n_cols, rowptr, edges, nnz, device, row_ids=None):
         self.n_rows, self.n_cols, self.nnz = n_rows, n_cols, nnz
         self.rowptr, self.edges, self.device = rowptr, edges, device
+        self.row_ids = row_ids
         self.transpose = None
         self.symmetric = None
         self._plans = {}
         self._rowptr_host = None
+        self._row_ids_host = None
 
     def rowptr_host(self):
+        """Row pointers in storage order (slots when degree-ordered)."""
         if self._rowptr_host is None:
             self._rowptr_host = self.rowptr.cpu().numpy()
         return self._rowptr_host
+
+    def row_ids_host(self):
+        if self.row_ids is None:
+            return None
+        if self._row_ids_host is None:
+            self._row_ids_host = self.row_ids.cpu().numpy()
+        return self._row_ids_host
 
     def hubs(self, threshold, chunk=None):
         chunk = chunk or DEFAULT_HUB_CHUNK
         key = (threshold, chunk)
         if key not in self._plans:
-            self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device)
+            self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device,
+                                         self.row_ids_host())
         return self._plans[key]
 
     def degrees(self):
-        return np.diff(self.rowptr_host().astype(np.int64))
+        """Degree of every row, indexed by row id."""
+        deg = np.diff(self.rowptr_host().astype(np.int64))
+        ids = self.row_ids_host()
+        if ids is None:
+            return deg
+        out = np.empty_like(deg)
+        out[ids] = deg
+        return out
+
+
+def order_by_degree(lib, g, stream):
+    """The same operator with its rows stored in degree-descending slots (lgcn_csr_order_by_degree):
+    lane groups of a wave then stream rows of equal length. Bitwise-neutral."""
+    n, nnz, dev = g.n_rows, g.nnz, g.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    deg_tmp, deg_sorted, iota = (torch.empty(max(n, 1), **i32) for _ in range(3))
+    row_ids = torch.empty(max(n, 1), **i32)
+    rowptr = torch.empty(n + 1, **i32)
+    edges = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+    nbytes = ctypes.c_size_t(0)
+    args = (_ptr(g.rowptr), _ptr(g.edges), n, nnz, _ptr(deg_tmp), _ptr(deg_sorted), _ptr(iota),
+            _ptr(row_ids), _ptr(rowptr), _ptr(edges))
+    _check(lib.lgcn_csr_order_by_degree(*args, None, ctypes.byref(nbytes), stream),
+           "lgcn_csr_order_by_degree(size)")
+    temp = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
+    _check(lib.lgcn_csr_order_by_degree(*args, _ptr(temp), ctypes.byref(nbytes), stream),
+           "lgcn_csr_order_by_degree")
+    del deg_tmp, deg_sorted, iota, temp
+    o = Graph(n, g.n_cols, rowptr, edges, nnz, dev, row_ids=row_ids[:n])
+    o.symmetric = g.symmetric
+    return o
 
 
 def _coo_to_csr(lib, key, other, vals, nnz, n_keys, device, stream, sort):
@@ -259,8 +321,10 @@ def _coo_to_csr(lib, key, other, vals, nnz, n_keys, device, stream, sort):
     return rowptr, edges
 
 
-def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, cols_sorted):
-    """Attach the backward operator: Â itself if bitwise symmetric, else a stably sorted Âᵀ."""
+def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, cols_sorted,
+                  order=None):
+    """Attach the backward operator: Â itself if bitwise symmetric, else a stably sorted Âᵀ;
+    then store both in the processing order (row_order())."""
     g = Graph(n, n, rowptr, edges, nnz, device)
     symmetric = False
     if cols_sorted:
@@ -269,13 +333,19 @@ def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, 
                                             stream), "lgcn_csr_check_symmetric")
         symmetric = int(asym.item()) == 0
     g.symmetric = symmetric
-    if symmetric:
-        g.transpose = g
-    else:
+    t = None
+    if not symmetric:
         # Âᵀ with each row's entries in Â's stored order (torch's sparse t() + addmm loop)
         t_rowptr, t_edges = _coo_to_csr(lib, cols, rows, vals, nnz, n, device, stream, sort=True)
-        g.transpose = Graph(n, n, t_rowptr, t_edges, nnz, device)
-        g.transpose.transpose = g
+        t = Graph(n, n, t_rowptr, t_edges, nnz, device)
+        t.symmetric = False
+    if row_order(order) == "degree":
+        g = order_by_degree(lib, g, stream)
+        t = order_by_degree(lib, t, stream) if t is not None else None
+    if t is None:
+        g.transpose = g
+    else:
+        g.transpose, t.transpose = t, g
     return g
 
 
@@ -380,7 +450,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
         partials = torch.empty(hp.n_slots * d, dtype=torch.float32, device=graph.device)
     stream = stream or _stream(graph.device)
     x = rows_desc(x_segments, d)
-    _check(lib.lgcn_spmm_layer(_ptr(graph.rowptr), _ptr(graph.edges), graph.n_rows,
+    _check(lib.lgcn_spmm_layer(_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids),
+                               graph.n_rows,
                                min(hp.threshold, INT32_MAX), _ptr(hp.items), hp.n_items,
                                _ptr(partials), x, x_div, _ptr(y), y.stride(0), d,
                                ctypes.byref(epi), stream), "lgcn_spmm_layer")

@@ -22,6 +22,10 @@
  *    (elements). Node ids follow main.py:283-287: users [0,U), items [U,U+I), brands [U+I,N).
  *  - CSR edge records are 8-byte {int32 col, fp32 val} pairs stored as int64 (lgcn_edge_t),
  *    rows keep the COO's stored order of their nonzeros (the order torch.sparse.mm sums them in).
+ *  - Processing order: the propagation entry points take an optional `row_ids` [n_rows]. When
+ *    it is non-NULL the CSR rows are stored in slots (lgcn_csr_order_by_degree): slot s holds
+ *    the edges of row row_ids[s] and its result is written to row row_ids[s]. Column ids, X, Y
+ *    and the epilogue operands are always in row-id space; only the work order changes.
  *  - Numerics: rows of degree <= hub_threshold are summed by one sequential fmaf chain in stored
  *    order, the exact arithmetic of ATen's addmm_sparse_dense_cpu loop that torch.sparse.mm runs
  *    on CPU (bitwise identical results). Rows above the threshold ("hubs") are cut into fixed
@@ -37,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 1
+#define LGCN_ABI_VERSION 2
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -70,7 +74,8 @@ typedef struct {
     int64_t ld;
 } lgcn_rows_t;
 
-/* hub work: one chunk of one long row -> one partial-sum slot of d floats */
+/* hub work: one chunk of one long row -> one partial-sum slot of d floats (beg/end index the
+ * edge array as stored, i.e. in slot order when the CSR is degree-ordered) */
 typedef struct {
     int32_t row;
     int32_t beg;
@@ -78,7 +83,7 @@ typedef struct {
     int32_t slot;
 } lgcn_hub_item_t;
 
-/* one long row: its partials occupy slots [first_slot, first_slot + n_slots) */
+/* one long row: its partials occupy slots [first_slot, first_slot + n_slots); row = output row */
 typedef struct {
     int32_t row;
     int32_t first_slot;
@@ -141,6 +146,16 @@ int lgcn_coo_sort_perm(const int64_t* keys, int64_t nnz, int32_t n_keys, int32_t
 int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
                              int64_t nnz, int32_t* asym, void* stream);
 
+/* Degree-ordered copy of a CSR for the propagation kernels: row_ids[s] = the row processed in
+ * slot s (degree descending, ties in row order: a stable radix sort), rowptr_out[n_rows+1] /
+ * edges_out[nnz] = the rows in slot order, each row's edges in their original order (so every
+ * result is bitwise unchanged). Scratch deg_tmp / deg_sorted / iota_tmp: n_rows int32 each.
+ * Two-call protocol for temp (temp == NULL: only *temp_bytes_host is written). */
+int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
+                             int64_t nnz, int32_t* deg_tmp, int32_t* deg_sorted, int32_t* iota_tmp,
+                             int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
+                             void* temp, size_t* temp_bytes_host, void* stream);
+
 /* ---- adjacency builder (main.py:313-336 on the device) -------------------------------------- */
 /* deg[r] = number of stored edges with row r (duplicates counted, main.py:326 rowsum of the
  * ones matrix), by binary search over the SORTED keys (keys_b of lgcn_adj_sort_unique). */
@@ -171,9 +186,10 @@ int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, in
  *    lgcn_hub_combine then finishes those rows. Both kinds run in ONE launch.
  * X is read through `x` (segments allowed); x_div = 1 reads it as is, otherwise every gathered
  * element is divided by x_div once (ADD epilogue only: the backward's G/(K+1)).
- * Y is [n_rows x ldy]. d in [1, 2048]. */
-int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
-                    int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
+ * Y is [n_rows x ldy]. d in [1, 2048]. row_ids: NULL, or the slot -> row map of a
+ * degree-ordered CSR (see Conventions). */
+int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                    int32_t n_rows, int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
                     float* partials, lgcn_rows_t x, float x_div, float* y, int64_t ldy, int32_t d,
                     const lgcn_epilogue_t* epi_host, void* stream);
 
@@ -190,7 +206,8 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
  * final = mean(E0..EK) into out [n x d]. emb = E0 segments. Hub plan as in lgcn_spmm_layer
  * (partials sized for it). ev_host: NULL or 2*K hipEvent_t recorded around each layer's
  * lgcn_spmm_layer launch (timing only). */
-int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
+                           const int32_t* row_ids, int32_t n,
                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
                            int32_t n_hub_rows, float* partials, lgcn_rows_t emb, int32_t d,
@@ -201,7 +218,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges, int3
  * (c = G/(K+1); h = c; K times h = c + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric).
  * G is read in place as segments (the user/item/brand output grads); c is never stored.
  * work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. */
-int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n,
+int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
+                            const int32_t* row_ids, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
                             int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out, int32_t d,

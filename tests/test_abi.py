@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == 1
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 2
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -53,24 +53,28 @@ def test_argument_validation_without_gpu(lib):
     ep.mode = 7
     rows = engine.RowsT()
     # bad epilogue / bad d / negative sizes return before any HIP call
-    assert lib.lgcn_spmm_layer(None, None, 0, 0, None, 0, None, rows, 1.0, None, 0, 64,
+    assert lib.lgcn_spmm_layer(None, None, None, 0, 0, None, 0, None, rows, 1.0, None, 0, 64,
                                ctypes.byref(ep), None) == -1
     ep.mode = engine.LGCN_EPI_STORE
-    assert lib.lgcn_spmm_layer(None, None, 10, 0, None, 0, None, rows, 1.0, None, 0, 0,
+    assert lib.lgcn_spmm_layer(None, None, None, 10, 0, None, 0, None, rows, 1.0, None, 0, 0,
                                ctypes.byref(ep), None) == -1
-    assert lib.lgcn_spmm_layer(None, None, -1, 0, None, 0, None, rows, 1.0, None, 0, 64,
+    assert lib.lgcn_spmm_layer(None, None, None, -1, 0, None, 0, None, rows, 1.0, None, 0, 64,
                                ctypes.byref(ep), None) == -1
-    assert lib.lgcn_spmm_layer(None, None, 0, 0, None, 0, None, rows, 0.0, None, 64, 64,
+    assert lib.lgcn_spmm_layer(None, None, None, 0, 0, None, 0, None, rows, 0.0, None, 64, 64,
                                ctypes.byref(ep), None) == -1
     ep.mode = engine.LGCN_EPI_MEAN
     ep.n_prev = 18
     ep.div = 2.0
     assert lib.lgcn_hub_combine(None, 0, None, None, 64, 64, ctypes.byref(ep), None) == -3
-    assert lib.lgcn_propagate_forward(None, None, 5, 0, None, 0, None, 0, None, rows, 64, -1,
+    assert lib.lgcn_propagate_forward(None, None, None, 5, 0, None, 0, None, 0, None, rows, 64, -1,
                                       None, None, None, None) == -1
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
                                   ctypes.byref(nbytes), None) == -1
+    assert lib.lgcn_csr_order_by_degree(None, None, -1, 0, None, None, None, None, None, None,
+                                        None, ctypes.byref(nbytes), None) == -1
+    assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, None, None, None, None, None, None,
+                                        ctypes.c_void_p(1), ctypes.byref(nbytes), None) == -1
 
 
 def test_struct_layout_matches_header():

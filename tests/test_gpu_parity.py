@@ -17,6 +17,16 @@ from util import assert_close_normwise, sha1
 
 pytestmark = pytest.mark.gpu
 
+# every parity test below that takes `order` runs on both CSR storage orders: rows in id order
+# and degree-ordered slots (the default). Results must be identical.
+ORDERS = pytest.mark.parametrize("order", ["degree", "stored"])
+
+
+@pytest.fixture
+def order(request, monkeypatch):
+    monkeypatch.setenv("LGCN_ROW_ORDER", request.param)
+    return request.param
+
 
 def _adj(z, dev):
     U, I, B, d, K = case_dims(z)
@@ -32,9 +42,10 @@ def _model(z, dev, fusion=False):
     return LightGCN(U, I, B, Cfg(d, K)).to(dev)
 
 
+@ORDERS
 @pytest.mark.parametrize("mode", ["exact", "default"])
 @pytest.mark.parametrize("name", CASES)
-def test_model_forward_backward_vs_reference(gpu_device, monkeypatch, name, mode):
+def test_model_forward_backward_vs_reference(gpu_device, monkeypatch, name, mode, order):
     if mode == "exact":
         monkeypatch.setenv("LGCN_HUB_THRESHOLD", "exact")
     z = load_case(name)
@@ -127,8 +138,9 @@ def _rand_graph(n, nnz, seed, symmetric=True):
     return r, c, v
 
 
+@ORDERS
 @pytest.mark.parametrize("d", [1, 3, 4, 12, 16, 32, 64, 100, 128, 256, 512])
-def test_dims_and_layers_bitwise(gpu_device, d):
+def test_dims_and_layers_bitwise(gpu_device, d, order):
     n = 700
     r, c, v = _rand_graph(n, 5000, d)
     for K in (0, 1, 3):
@@ -160,7 +172,8 @@ def test_segments_and_misaligned_rows(gpu_device):
     assert np.array_equal(engine.propagate_forward(gr, [mis], 3).cpu().numpy(), want)
 
 
-def test_unsorted_coo_with_duplicates(gpu_device):
+@ORDERS
+def test_unsorted_coo_with_duplicates(gpu_device, order):
     """Arbitrary stored order + duplicate coordinates: the stable sort keeps torch's per-row
     order, so results stay bitwise = torch.sparse.mm on that COO (oracle)."""
     rng = np.random.default_rng(2)
@@ -182,7 +195,8 @@ def test_unsorted_coo_with_duplicates(gpu_device):
     assert np.array_equal(gb, oracle.backward(r, c, v, G, 2))
 
 
-def test_hub_rows_chunked_vs_exact(gpu_device):
+@ORDERS
+def test_hub_rows_chunked_vs_exact(gpu_device, order):
     """A 20k-edge hub row: chunked (default) within tolerance, exact mode bitwise; both
     deterministic run to run."""
     rng = np.random.default_rng(3)
@@ -209,6 +223,36 @@ def test_hub_rows_chunked_vs_exact(gpu_device):
     assert g.hubs(256).n_rows >= 1
 
 
+def test_degree_order_plan(gpu_device):
+    """lgcn_csr_order_by_degree: row_ids is a permutation, slots hold degrees in descending order
+    with ties in row-id order (stable), each slot's edges are its row's edges in stored order,
+    and the hub plan's output rows are row ids."""
+    z = load_case("hub_d32")
+    adj = _adj(z, gpu_device)
+    g = engine.graph_from_coo(adj)
+    assert g.row_ids is not None
+    ids = g.row_ids_host()
+    n = g.n_rows
+    assert np.array_equal(np.sort(ids), np.arange(n))
+    rp_s = g.rowptr_host().astype(np.int64)
+    deg_s = np.diff(rp_s)
+    r = z["adj_row"].astype(np.int64)
+    rp = np.searchsorted(r, np.arange(n + 1))
+    deg = np.diff(rp)
+    assert np.array_equal(deg_s, deg[ids])
+    assert np.array_equal(ids, np.lexsort((np.arange(n), -deg)))
+    e = g.edges.cpu().numpy()
+    want = engine.pack_edges(z["adj_col"], z["adj_val"])
+    for s in np.random.default_rng(0).choice(n, 50, replace=False):
+        row = ids[s]
+        assert np.array_equal(e[rp_s[s]:rp_s[s + 1]], want[rp[row]:rp[row + 1]])
+    assert np.array_equal(g.degrees(), deg)
+    hp = g.hubs(16)
+    hub_rows = hp.rows.cpu().numpy()[:, 0]
+    assert hub_rows.size > 0
+    assert np.array_equal(np.sort(hub_rows), np.sort(np.nonzero(deg > 16)[0]))
+
+
 def test_empty_graph_and_isolated_rows(gpu_device):
     n, d = 10, 16
     adj = torch.sparse_coo_tensor(torch.zeros((2, 0), dtype=torch.int64), torch.zeros(0),
@@ -227,7 +271,8 @@ def test_plan_cache_reused_and_invalidated(gpu_device):
     assert engine.graph_from_coo(adj) is not g1
 
 
-def test_c2_scale_uniform_and_powerlaw(gpu_device):
+@ORDERS
+def test_c2_scale_uniform_and_powerlaw(gpu_device, order):
     """BASELINE configs[1] shapes (50k x 50k, 1M interactions, d=64, K=3): exact mode bitwise,
     default mode within tolerance, forward and backward."""
     for gen in ("uniform", "powerlaw"):
@@ -256,7 +301,8 @@ def test_c2_scale_uniform_and_powerlaw(gpu_device):
         assert_close_normwise(gb, oracle.backward(r, c, v, G, 3), what=gen + " bwd")
 
 
-def test_dist_rowpart_and_featsplit_kernels_on_gpu(gpu_device):
+@ORDERS
+def test_dist_rowpart_and_featsplit_kernels_on_gpu(gpu_device, order):
     """The distributed decompositions' GPU local layers, for every rank of a P=3 partition,
     driven in one process with the all-gather emulated by copies: the assembled result is
     bitwise the single-GPU / oracle result (exact mode), for both rowpart and featsplit."""

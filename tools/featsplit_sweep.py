@@ -1,0 +1,108 @@
+"""Per-rank cost of the featsplit decomposition, measured on ONE GPU: at P ranks every rank runs
+the full K-layer propagation over the whole C3 graph on d/P columns, with no exchange. Timing
+the single-GPU forward at d = 64/P for P in 1, 2, 4, 8 predicts the strong-scaling curve of
+`bench.py --gpus P --mode featsplit` (the ranks do not share anything but the node's power).
+
+    python tools/featsplit_sweep.py [--config c3] [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from gcn_recommendation_amd import engine  # noqa: E402
+
+
+def relabel(rowptr, c, v, U, I, order):
+    """Node relabelling experiment: returns (rowptr', c', v') of P·Â·Pᵀ with every row's edges
+    kept in their stored order (so each output row is the same fp32 chain, bitwise)."""
+    n = U + I
+    deg = np.diff(rowptr).astype(np.int64)
+    if order in ("degree", "degree_rows"):
+        perm = np.argsort(-deg, kind="stable")
+    elif order == "cluster":
+        # items by popularity first; then users grouped by their least popular item, so an item
+        # row's users sit in consecutive ids (4 rows of d=8 per 128-B line)
+        items = U + np.argsort(-deg[U:], kind="stable")
+        new_item = np.empty(n, np.int64)
+        new_item[items] = np.arange(I)
+        ue = c[:rowptr[U]].astype(np.int64)
+        key = np.full(U, -1, np.int64)
+        has = deg[:U] > 0
+        key[has] = np.maximum.reduceat(new_item[ue], rowptr[:U][has].astype(np.int64))
+        users = np.argsort(key, kind="stable")
+        perm = np.concatenate([items, users])
+    else:
+        return rowptr, c, v
+    new_id = np.empty(n, np.int64)
+    new_id[perm] = np.arange(n)
+    dn = deg[perm]
+    rp = np.zeros(n + 1, np.int64)
+    np.cumsum(dn, out=rp[1:])
+    idx = np.arange(rp[-1], dtype=np.int64) - np.repeat(rp[:-1], dn) + \
+        np.repeat(rowptr[:-1][perm].astype(np.int64), dn)
+    if order == "degree_rows":  # processing order only: columns stay in the original ids
+        return rp.astype(np.int32), c[idx], v[idx]
+    return rp.astype(np.int32), new_id[c[idx]].astype(np.int32), v[idx]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--gen", default="powerlaw")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--dims", default="64,32,16,8")
+    ap.add_argument("--order", default="none", choices=["none", "degree", "degree_rows", "cluster"])
+    args = ap.parse_args()
+    cfg = bench.CONFIGS[args.config]
+    dev = torch.device("cuda", 0)
+    engine.load_library()
+    r, c, v, _, _, _ = bench.make_graph(cfg, args.gen, 16)
+    U, I = cfg["users"], cfg["items"]
+    n, K, nnz = U + I, cfg["K"], len(v)
+    rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
+    rowptr, c, v = relabel(rowptr, c, v, U, I, args.order)
+    g = engine.graph_from_host_csr(rowptr, c, v, n, dev)
+    thr = engine.hub_threshold_from_env()
+    g.hubs(thr)
+    out = []
+    for d in [int(x) for x in args.dims.split(",")]:
+        gen = torch.Generator().manual_seed(42)
+        segs = [bench.xavier(U, d, gen).to(dev), bench.xavier(I, d, gen).to(dev)]
+        for _ in range(3):
+            engine.propagate_forward(g, segs, K, thr)
+        torch.cuda.synchronize()
+        evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(K)] for _ in range(args.steps)]
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for s in range(args.steps):
+            engine.propagate_forward(g, segs, K, thr, layer_events=evs[s])
+        b.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / args.steps
+        lay = np.array([[x.elapsed_time(y) for x, y in st] for st in evs]).mean(0)
+        b_layer = nnz * (4 * d + 8) + 4 * (n + 1) + 4 * n * d
+        p = 64 // d
+        row = {"order": args.order, "d": d, "ranks_at_d64": p, "ms_per_step": round(ms, 3),
+               "per_layer_ms": [round(float(x), 3) for x in lay],
+               "store_layer_GBps": round(b_layer / (lay[:-1].mean() / 1e3) / 1e9, 1),
+               "edges_per_s": round(K * nnz / (ms / 1e3), 1)}
+        out.append(row)
+        print(json.dumps(row), flush=True)
+        del segs
+        torch.cuda.empty_cache()
+    base = out[0]["ms_per_step"]
+    print(json.dumps({"predicted_featsplit_speedup": {
+        str(r_["ranks_at_d64"]): round(base / r_["ms_per_step"], 2) for r_ in out}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

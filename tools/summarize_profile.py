@@ -43,7 +43,10 @@ def main(prof, tag, rnd, algo_bytes):
                           "hbm_bytes_per_launch": int((2 * v["FETCH_SIZE_KB_avg"]
                                                        + v["WRITE_SIZE_KB_avg"]) * 1024),
                           **v}
-    store = [k for k in kernels if "k_layer" in k and ", 0, " in k.split("16, 1")[-1][:4]]
+    def layer_mode(k):  # k_layer<V, G, NV, MODE, RPG, U, NP, XD>
+        args = k.split("k_layer<", 1)[1].split(">, ", 1)[1].rstrip(">").split(", ")
+        return int(args[2])
+    store = [k for k in kernels if "k_layer" in k and layer_mode(k) == 0]
     store = store or [k for k in kernels if "k_layer" in k]
     dom = max(store, key=lambda k: (kernels[k]["avg_ms"] or 0) * (kernels[k]["calls"] or 0))
     out = {"command": f"tools/profile.sh {tag} ... (see profiles/README.md)",
