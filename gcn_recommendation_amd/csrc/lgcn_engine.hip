@@ -514,6 +514,16 @@ __global__ void k_csr_gather_rows(const int32_t* __restrict__ rowptr_out,
     edges_out[j] = edges[rowptr[row_ids[lo]] + (j - rowptr_out[lo])];
 }
 
+// edges_out[j] = edges[j] with its column id c replaced by new_id[c] (value bits kept)
+__global__ void k_csr_relabel_cols(const lgcn_edge_t* __restrict__ edges, int64_t nnz,
+                                   const int32_t* __restrict__ new_id,
+                                   lgcn_edge_t* __restrict__ edges_out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    const int2 e = load_edge(edges + j);
+    edges_out[j] = (lgcn_edge_t)(((uint64_t)(uint32_t)e.y << 32) | (uint32_t)new_id[e.x]);
+}
+
 // ---------------------------------------------------------------------------------------------
 // adjacency builder (main.py:313-336 on the device): degree histogram, duplicate merge by a
 // 64-bit radix sort of row*n+col keys + run-length encode, values fp32((d_r * m) * d_c)
@@ -668,8 +678,7 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_
                    const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                    const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
                    const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
-    // one row per group (deep unroll) for the MEAN epilogue, whose reads of E0..E_{K-1} would
-    // otherwise serialise inside a row stream; row bundles (shallow unroll) everywhere else
+    // one row per group (deep unroll) on small graphs, row bundles (shallow unroll) otherwise
     constexpr int U1 = NV >= 8 ? 1 : 8 / NV;
     constexpr int UB = NV >= 4 ? 1 : 4 / NV;
     constexpr int RB = G >= 16 ? 15 : G - 1;
@@ -681,18 +690,18 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_
         LGCN_V(15, 8)
 #undef LGCN_V
     }
-    if (ep.mode == LGCN_EPI_MEAN) {
-        if (NV <= 2 && g_rows_per_group == 0) {  // early-issued E0..E_{K-1} row loads
+    // keep >= ~64k lane groups in the grid: small graphs (the reference's real datasets) run
+    // one row per group, Books-scale graphs 15-row bundles (with degree-ordered slots the rows
+    // of a bundle have equal length, which also pays for the MEAN epilogue's row reads)
+    const int64_t per = (int64_t)n_rows / 65536;
+    if (RB <= 1 || g_rows_per_group == 1 || per < 2) {
+        if (ep.mode == LGCN_EPI_MEAN && NV <= 2) {  // early-issued E0..E_{K-1} row loads
             if (ep.n_prev == 2) return launch_layer_rpg<V, G, NV, 1, U1, 2>(LGCN_ARGS);
             if (ep.n_prev == 3) return launch_layer_rpg<V, G, NV, 1, U1, 3>(LGCN_ARGS);
             if (ep.n_prev == 4) return launch_layer_rpg<V, G, NV, 1, U1, 4>(LGCN_ARGS);
         }
         return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
     }
-    if (RB <= 1 || g_rows_per_group == 1) return launch_layer_rpg<V, G, NV, 1, U1>(LGCN_ARGS);
-    // keep >= ~64k lane groups in the grid: small graphs (the reference's real datasets) run
-    // one row per group, Books-scale graphs 15-row bundles
-    const int64_t per = (int64_t)n_rows / 65536;
     if (per >= RB) return launch_layer_rpg<V, G, NV, RB, UB>(LGCN_ARGS);
     if constexpr (RB >= 8) {
         if (per >= 8) return launch_layer_rpg<V, G, NV, 8, UB>(LGCN_ARGS);
@@ -1013,6 +1022,15 @@ int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, in
     if (nnz == 0) return 0;
     hipLaunchKernelGGL(k_csr_gather_rows, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, s, rowptr_out, row_ids, rowptr, edges, n, nnz, edges_out);
+    return last_err();
+}
+
+int lgcn_csr_relabel_cols(const lgcn_edge_t* edges, int64_t nnz, const int32_t* new_id,
+                          lgcn_edge_t* edges_out, void* stream) {
+    if (nnz < 0 || (nnz > 0 && (!edges || !new_id || !edges_out))) return LGCN_EINVAL;
+    if (nnz == 0) return 0;
+    hipLaunchKernelGGL(k_csr_relabel_cols, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, S(stream), edges, nnz, new_id, edges_out);
     return last_err();
 }
 

