@@ -202,7 +202,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # LGCN_SHARED_GPU=1 (with LGCN_DIST_BACKEND=gloo): every rank on cuda:0 — a rehearsal of
+    # the N > 1 path on a one-GPU box; the numbers it prints are not a scaling measurement
+    local_rank = 0 if os.environ.get("LGCN_SHARED_GPU") else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     cfg = CONFIGS[args.config]
@@ -335,9 +337,29 @@ def main():
     e.record()
     torch.cuda.synchronize()
     bwd_ms = a.elapsed_time(e) / args.steps
+    # the upstream gradient of one BPR batch (main.py:496-497: 2048 users, 2048 pos + 2048 neg
+    # items): row-sparse, so the masked backward gathers only its live rows in layer 1
+    rs = np.random.default_rng(1)
+    for t in gsegs:
+        t.zero_()
+    gsegs[0][torch.from_numpy(rs.integers(0, U, 2048)).to(dev)] = 1e-3
+    gsegs[1][torch.from_numpy(rs.integers(0, I, 4096)).to(dev)] = -1e-3
+    for _ in range(2):
+        engine.propagate_backward(g, gsegs, K, hub_thr)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(args.steps):
+        engine.propagate_backward(g, gsegs, K, hub_thr)
+    e.record()
+    torch.cuda.synchronize()
+    bpr_ms = a.elapsed_time(e) / args.steps
     result["backward"] = {"ms_per_step": round(bwd_ms, 4),
                           "propagated_edges_per_s": round(K * nnz / (bwd_ms / 1e3), 1),
-                          "what": "dE0 = sum_k (Â^T)^k G/(K+1), Horner order, G read in place"}
+                          "what": "dE0 = sum_k (Â^T)^k G/(K+1), Horner order, G read in place "
+                                  "(dense G)",
+                          "bpr_batch_G_ms_per_step": round(bpr_ms, 4),
+                          "bpr_batch_G": "G = a BPR batch's output gradient (<= 6144 live rows): "
+                                         "row-sparse path (lgcn_rows_nonzero mask)"}
     del gsegs
 
     if not fusion:

@@ -91,26 +91,40 @@ __host__ __device__ __forceinline__ bool is_pow2f(float x) {
     return x > 0.f && frexpf(x, &e) == 0.5f;
 }
 
-// XD: 0 = gather X as is, 1 = X / xdiv (IEEE division), 2 = X * xdiv where the host already
-// replaced a power-of-two divisor by its (exact) reciprocal
+// XD & 3: 0 = gather X as is, 1 = X / xdiv (IEEE division), 2 = X * xdiv where the host
+// already replaced a power-of-two divisor by its (exact) reciprocal.
+// XD & 4: X is row-sparse; x_nz is a bitmask of its rows that hold a nonzero. Edges into an
+// all-zero row are skipped: fma(v, ±0, acc) == acc for every acc a chain can hold (a chain
+// starts at +0 and never reaches -0), so the result is bitwise that of the dense chain.
 template <typename V, int XD>
 __device__ __forceinline__ V load_x(const float* p, float xdiv) {
     const V v = VT<V>::load(p);
-    if constexpr (XD == 1) return VT<V>::div(v, xdiv);  // gathered operand = X / xdiv, rounded once
-    else if constexpr (XD == 2) return mul_s<V>(v, xdiv);  // host passes 1/xdiv (exact)
+    if constexpr ((XD & 3) == 1) return VT<V>::div(v, xdiv);  // X / xdiv, rounded once
+    else if constexpr ((XD & 3) == 2) return mul_s<V>(v, xdiv);  // host passes 1/xdiv (exact)
     else return v;
+}
+
+__device__ __forceinline__ bool row_live(const uint32_t* __restrict__ nz, int32_t r) {
+    return (nz[r >> 5] >> (r & 31)) & 1u;
 }
 
 template <typename V, int G, int NV, int U, int XD = 0>
 __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges, int32_t beg,
                                            int32_t end, const lgcn_rows_t& x, int lane, int dW,
-                                           V (&acc)[NV], float xdiv = 1.f) {
+                                           V (&acc)[NV], float xdiv = 1.f,
+                                           const uint32_t* __restrict__ x_nz = nullptr) {
     using T = VT<V>;
     for (int32_t j = beg; j < end; j += U) {
         const int n = min(U, end - j);
         int2 e[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) e[u] = (u < n) ? load_edge(edges + j + u) : make_int2(0, 0);
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (XD & 4) live[u] = u < n && row_live(x_nz, e[u].x);
+            else live[u] = u < n;
+        }
         V xv[U][NV];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -118,12 +132,12 @@ __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int c = lane + q * G;
-                xv[u][q] = (u < n && c < dW) ? load_x<V, XD>(rp + c * T::W, xdiv) : T::zero();
+                xv[u][q] = (live[u] && c < dW) ? load_x<V, XD>(rp + c * T::W, xdiv) : T::zero();
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (u < n) {
+            if (live[u]) {
                 const float v = __int_as_float(e[u].y);
 #pragma unroll
                 for (int q = 0; q < NV; ++q) acc[q] = T::fma(v, xv[u][q], acc[q]);
@@ -152,8 +166,11 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
             s = T::add(s, out);
             out = div_exact<V>(s, ep.div, ep.pad);
         } else if constexpr (MODE == LGCN_EPI_ADD) {
-            // Horner step: (Z / div) + Â·X, Z read in place (segments), Z / div rounded once
-            out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div, ep.pad), out);
+            // Horner step: (Z / div) + Â·X, Z read in place (segments), Z / div rounded once.
+            // A row outside addend_nz is all ±0: ±0/div + out == out (out is never -0).
+            if (!ep.addend_nz || row_live(ep.addend_nz, row))
+                out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div,
+                                          ep.pad), out);
         }
         T::store(yr + c * T::W, out);
     }
@@ -173,7 +190,8 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                                             const int32_t* __restrict__ row_ids, int32_t n_rows,
                                             int32_t hub_thr, int32_t r0, const lgcn_rows_t& x,
                                             float* __restrict__ y, int64_t ldy, int lane, int dW,
-                                            const lgcn_epilogue_t& ep, float xdiv) {
+                                            const lgcn_epilogue_t& ep, float xdiv,
+                                            const uint32_t* __restrict__ x_nz) {
     using T = VT<V>;
     static_assert(RPG < G, "row boundaries are held one per lane");
     const int nrows = min(RPG, n_rows - r0);
@@ -241,6 +259,12 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                 ++cnt;
             }
         }
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (XD & 4) live[u] = u < cnt && row_live(x_nz, col[u]);
+            else live[u] = u < cnt;
+        }
         V xv[U][NV];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -248,15 +272,17 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int c = lane + q * G;
-                xv[u][q] = (u < cnt && c < dW) ? load_x<V, XD>(rp + c * T::W, xdiv) : T::zero();
+                xv[u][q] = (live[u] && c < dW) ? load_x<V, XD>(rp + c * T::W, xdiv) : T::zero();
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (u < cnt) {
                 while (fr < rid[u]) flush(fr++);
+                if (live[u]) {
 #pragma unroll
-                for (int q = 0; q < NV; ++q) acc[q] = T::fma(val[u], xv[u][q], acc[q]);
+                    for (int q = 0; q < NV; ++q) acc[q] = T::fma(val[u], xv[u][q], acc[q]);
+                }
             }
         }
         if (cnt < U) break;
@@ -288,7 +314,8 @@ __global__ __launch_bounds__(kBlock) void k_layer(
     const int32_t* __restrict__ row_ids, int32_t n_rows,
     int32_t hub_thr, const lgcn_hub_item_t* __restrict__ items, int32_t n_items,
     int32_t hub_blocks, float* __restrict__ partials, lgcn_rows_t x, float* __restrict__ y,
-    int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep, float xdiv) {
+    int64_t ldy, int32_t d, int32_t dW, lgcn_epilogue_t ep, float xdiv,
+    const uint32_t* __restrict__ x_nz) {
     using T = VT<V>;
     constexpr int RPB = kBlock / G;
     const int lane = threadIdx.x & (G - 1);
@@ -302,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
         constexpr int UH = NV >= 8 ? 1 : 8 / NV;  // hub chunks are long: deep unroll
-        accumulate<V, G, NV, UH, XD>(edges, w.beg, w.end, x, lane, dW, acc, xdiv);
+        accumulate<V, G, NV, UH, XD>(edges, w.beg, w.end, x, lane, dW, acc, xdiv, x_nz);
         float* pr = partials + (int64_t)w.slot * d;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -325,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
         if constexpr (MODE == LGCN_EPI_MEAN && NP > 0) {
             V pre[NP][NV];
             mean_prefetch<V, G, NV, NP>(ep, row, lane, dW, pre);
-            accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv);
+            accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv, x_nz);
             float* yr = y + (int64_t)row * ldy;
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
@@ -337,14 +364,15 @@ __global__ __launch_bounds__(kBlock) void k_layer(
                 T::store(yr + c * T::W, div_exact<V>(T::add(s, acc[q]), ep.div, ep.pad));
             }
         } else {
-            accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv);
+            accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv, x_nz);
             epilogue_store<V, G, NV, MODE>(ep, row, lane, dW, acc, y, ldy);
         }
     } else {
         const int64_t r0 = gidx * RPG;
         if (r0 >= n_rows) return;
         rows_bundle<V, G, NV, MODE, RPG, U, XD>(rowptr, edges, row_ids, n_rows, hub_thr,
-                                                (int32_t)r0, x, y, ldy, lane, dW, ep, xdiv);
+                                                (int32_t)r0, x, y, ldy, lane, dW, ep, xdiv,
+                                                x_nz);
     }
 }
 
@@ -410,6 +438,53 @@ __global__ __launch_bounds__(kBlock) void k_scale_rows(lgcn_rows_t x, int32_t n_
     for (int q = 0; q < NV; ++q) {
         const int c = lane + q * G;
         if (c < dW) T::store(y + (int64_t)row * ldy + c * T::W, T::div(T::load(xr + c * T::W), div));
+    }
+}
+
+// Row-sparsity mask of a block: bit r of mask = row r holds a value != 0 (NaN counts). A block
+// owns 256 rows = 8 mask words (plain stores, no global atomics); one atomicAdd per block
+// accumulates the live-row count.
+template <typename V, int G, int NV>
+__global__ __launch_bounds__(kBlock) void k_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t dW,
+                                                         uint32_t* __restrict__ mask,
+                                                         int32_t* __restrict__ count) {
+    using T = VT<V>;
+    constexpr int RPB = kBlock / G;          // rows per pass
+    constexpr int ROWS = 256;                // rows per block
+    __shared__ uint32_t words[ROWS / 32];
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = threadIdx.x / G;
+    if (threadIdx.x < ROWS / 32) words[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * ROWS;
+    for (int i = grp; i < ROWS; i += RPB) {
+        const int64_t r = base + i;
+        bool nz = false;
+        if (r < n_rows) {
+            const float* xr = seg_row(x, (int32_t)r);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int c = lane + q * G;
+                if (c < dW) {
+                    const V v = T::load(xr + c * T::W);
+                    if constexpr (T::W == 4) nz |= !(v.x == 0.f && v.y == 0.f && v.z == 0.f && v.w == 0.f);
+                    else nz |= !(v == 0.f);
+                }
+            }
+        }
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) nz |= __shfl_xor((int)nz, o, G) != 0;
+        if (lane == 0 && nz) atomicOr(&words[i >> 5], 1u << (i & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < ROWS / 32) {
+        const int64_t w = (int64_t)blockIdx.x * (ROWS / 32) + threadIdx.x;
+        if (w * 32 < n_rows) mask[w] = words[threadIdx.x];
+        const int c = __popc(words[threadIdx.x]);
+        int t = c;
+#pragma unroll
+        for (int o = 4; o > 0; o >>= 1) t += __shfl_xor(t, o, 8);
+        if (threadIdx.x == 0 && t) atomicAdd(count, t);
     }
 }
 
@@ -629,7 +704,7 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, const int3
                      int32_t n_rows, int32_t thr,
                      const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                      const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
-                     const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
+                     const lgcn_epilogue_t& ep, float xdiv, const uint32_t* x_nz, hipStream_t s) {
     constexpr int RPB = kBlock / G;
     const int32_t hub_blocks = (n_items + RPB - 1) / RPB;
     const int64_t row_groups = ((int64_t)n_rows + RPG - 1) / RPG;
@@ -637,38 +712,36 @@ int launch_layer_rpg(const int32_t* rowptr, const lgcn_edge_t* edges, const int3
     const int64_t grid = hub_blocks + row_blocks;
     if (grid == 0) return 0;
     if (grid > 0x7fffffffLL) return LGCN_EINVAL;
+    // gather scaling and row-sparse X exist for the backward (ADD) only
+    if (ep.mode != LGCN_EPI_ADD && (xdiv != 1.f || x_nz)) return LGCN_EINVAL;
+#define LGCN_LAUNCH(MODE_, NP_, XD_, XDIV_)                                                      \
+    hipLaunchKernelGGL((k_layer<V, G, NV, MODE_, RPG, U, NP_, XD_>), dim3((uint32_t)grid),       \
+                       dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,  \
+                       hub_blocks, partials, x, y, ldy, d, dW, ep, XDIV_, x_nz)
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            if (xdiv != 1.f) return LGCN_EINVAL;  // gather scaling exists for the backward only
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_STORE, RPG, U>), dim3((uint32_t)grid),
-                               dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,
-                               hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
+            LGCN_LAUNCH(LGCN_EPI_STORE, 0, 0, 1.f);
             break;
         case LGCN_EPI_MEAN:
-            if (xdiv != 1.f) return LGCN_EINVAL;
-            hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_MEAN, RPG, U, NP>), dim3((uint32_t)grid),
-                               dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,
-                               hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
+            LGCN_LAUNCH(LGCN_EPI_MEAN, NP, 0, 1.f);
             break;
-        case LGCN_EPI_ADD:
-            if (xdiv != 1.f && is_pow2f(xdiv))
-                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 2>),
-                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows,
-                                   thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
-                                   1.0f / xdiv);
-            else if (xdiv != 1.f)
-                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U, 0, 1>),
-                                   dim3((uint32_t)grid), dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows,
-                                   thr, items, n_items, hub_blocks, partials, x, y, ldy, d, dW, ep,
-                                   xdiv);
-            else
-                hipLaunchKernelGGL((k_layer<V, G, NV, LGCN_EPI_ADD, RPG, U>), dim3((uint32_t)grid),
-                                   dim3(kBlock), 0, s, rowptr, edges, row_ids, n_rows, thr, items, n_items,
-                                   hub_blocks, partials, x, y, ldy, d, dW, ep, 1.f);
+        case LGCN_EPI_ADD: {
+            const int xd = (xdiv == 1.f ? 0 : is_pow2f(xdiv) ? 2 : 1) | (x_nz ? 4 : 0);
+            const float xa = (xd & 3) == 2 ? 1.0f / xdiv : xdiv;
+            switch (xd) {
+                case 0: LGCN_LAUNCH(LGCN_EPI_ADD, 0, 0, xa); break;
+                case 1: LGCN_LAUNCH(LGCN_EPI_ADD, 0, 1, xa); break;
+                case 2: LGCN_LAUNCH(LGCN_EPI_ADD, 0, 2, xa); break;
+                case 4: LGCN_LAUNCH(LGCN_EPI_ADD, 0, 4, xa); break;
+                case 5: LGCN_LAUNCH(LGCN_EPI_ADD, 0, 5, xa); break;
+                default: LGCN_LAUNCH(LGCN_EPI_ADD, 0, 6, xa); break;
+            }
             break;
+        }
         default:
             return LGCN_EINVAL;
     }
+#undef LGCN_LAUNCH
     return last_err();
 }
 
@@ -677,12 +750,13 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_
                    int32_t n_rows, int32_t thr,
                    const lgcn_hub_item_t* items, int32_t n_items, float* partials,
                    const lgcn_rows_t& x, float* y, int64_t ldy, int32_t d, int32_t dW,
-                   const lgcn_epilogue_t& ep, float xdiv, hipStream_t s) {
+                   const lgcn_epilogue_t& ep, float xdiv, const uint32_t* x_nz,
+                   hipStream_t s) {
     // one row per group (deep unroll) on small graphs, row bundles (shallow unroll) otherwise
     constexpr int U1 = NV >= 8 ? 1 : 8 / NV;
     constexpr int UB = NV >= 4 ? 1 : 4 / NV;
     constexpr int RB = G >= 16 ? 15 : G - 1;
-#define LGCN_ARGS rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, xdiv, s
+#define LGCN_ARGS rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, x, y, ldy, d, dW, ep, xdiv, x_nz, s
     if constexpr (VT<V>::W == 4 && G == 16 && NV == 1) {  // d = 64: explicit variants (lgcn_tune)
 #define LGCN_V(R_, U_) \
         if (g_rows_per_group == R_ && g_unroll == U_) return launch_layer_rpg<V, G, NV, R_, U_>(LGCN_ARGS);
@@ -796,10 +870,11 @@ int check_epi(const lgcn_epilogue_t* ep) {
 struct LayerF {
     const int32_t* rowptr; const lgcn_edge_t* edges; const int32_t* row_ids; int32_t n_rows, thr;
     const lgcn_hub_item_t* items; int32_t n_items; float* partials; const lgcn_rows_t* x;
-    float* y; int64_t ldy; int32_t d, dW; const lgcn_epilogue_t* ep; float xdiv; hipStream_t s;
+    float* y; int64_t ldy; int32_t d, dW; const lgcn_epilogue_t* ep; float xdiv;
+    const uint32_t* x_nz; hipStream_t s;
     template <typename V, int G, int NV> int operator()() const {
-        return launch_layer_t<V, G, NV>(rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, *x,
-                                        y, ldy, d, dW, *ep, xdiv, s);
+        return launch_layer_t<V, G, NV>(rowptr, edges, row_ids, n_rows, thr, items, n_items,
+                                        partials, *x, y, ldy, d, dW, *ep, xdiv, x_nz, s);
     }
 };
 
@@ -815,6 +890,17 @@ struct ScaleF {
     const lgcn_rows_t* x; int32_t n; int32_t dW; float div; float* y; int64_t ldy; hipStream_t s;
     template <typename V, int G, int NV> int operator()() const {
         return launch_scale_t<V, G, NV>(*x, n, dW, div, y, ldy, s);
+    }
+};
+
+struct NonzeroF {
+    const lgcn_rows_t* x; int32_t n; int32_t dW; uint32_t* mask; int32_t* count; hipStream_t s;
+    template <typename V, int G, int NV> int operator()() const {
+        const int64_t grid = ((int64_t)n + 255) / 256;
+        if (grid == 0) return 0;
+        hipLaunchKernelGGL((k_rows_nonzero<V, G, NV>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+                           *x, n, dW, mask, count);
+        return last_err();
     }
 };
 
@@ -834,13 +920,13 @@ int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
                int32_t n_rows, int32_t thr,
                const lgcn_hub_item_t* items, int32_t n_items, float* partials, lgcn_rows_t x,
                float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep_in, float xdiv,
-               hipStream_t s) {
+               const uint32_t* x_nz, hipStream_t s) {
     const lgcn_epilogue_t ep = with_pow2(ep_in);
     const bool vec_ok = rows_aligned(x) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep) &&
                         (n_items == 0 || al16(partials));
     const Geo g = pick_geo(d, vec_ok);
-    LayerF f{rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW, &ep,
-             xdiv, s};
+    LayerF f{rowptr, edges, row_ids, n_rows, thr, items, n_items, partials, &x, y, ldy, d, g.dW,
+             &ep, xdiv, x_nz, s};
     return dispatch_geo(g, f);
 }
 
@@ -1097,15 +1183,26 @@ int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, in
 
 int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
                     int32_t n_rows, int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
-                    float* partials, lgcn_rows_t x, float x_div, float* y, int64_t ldy, int32_t d,
-                    const lgcn_epilogue_t* epi_host, void* stream) {
+                    float* partials, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
+                    int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* stream) {
     if (int e = valid_geom(n_rows, d)) return e;
     if (int e = check_epi(epi_host)) return e;
     if (n_rows > 0 && (!rowptr || !y || ldy < d)) return LGCN_EINVAL;
     if (n_hub_items < 0 || (n_hub_items > 0 && (!hub_items || !partials))) return LGCN_EINVAL;
     if (!(x_div > 0.f)) return LGCN_EINVAL;
-    return spmm_layer(rowptr, edges, row_ids, n_rows, hub_threshold, hub_items, n_hub_items, partials, x, y,
-                      ldy, d, *epi_host, x_div, S(stream));
+    return spmm_layer(rowptr, edges, row_ids, n_rows, hub_threshold, hub_items, n_hub_items,
+                      partials, x, y, ldy, d, *epi_host, x_div, x_nz, S(stream));
+}
+
+int lgcn_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t d, uint32_t* mask, int32_t* count,
+                      void* stream) {
+    if (int e = valid_geom(n_rows, d)) return e;
+    if (!count || (n_rows > 0 && !mask)) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (int e = herr(hipMemsetAsync(count, 0, sizeof(int32_t), s))) return e;
+    const Geo g = pick_geo(d, rows_aligned(x));
+    NonzeroF f{&x, n_rows, g.dW, mask, count, s};
+    return dispatch_geo(g, f);
 }
 
 int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
@@ -1156,8 +1253,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1)], s))) return e;
         }
-        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items, partials, x,
-                               y, d, d, ep, 1.f, s))
+        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items,
+                               partials, x, y, d, d, ep, 1.f, nullptr, s))
             return e;
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1) + 1], s))) return e;
@@ -1171,8 +1268,9 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const int32_t* row_ids, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out, int32_t d,
-                            int32_t K, float* work_h, float* grad_e0, void* stream) {
+                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out,
+                            const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
+                            float* grad_e0, void* stream) {
     if (int e = valid_geom(n, d)) return e;
     if (K < 0 || !grad_out.p0 || !grad_e0) return LGCN_EINVAL;
     hipStream_t s = S(stream);
@@ -1185,17 +1283,20 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
     memset(&ep, 0, sizeof(ep));
     ep.mode = LGCN_EPI_ADD;
     ep.addend = grad_out;
+    ep.addend_nz = grad_nz;
     ep.div = div;
     lgcn_rows_t h = grad_out;
     float xdiv = div;
+    const uint32_t* x_nz = grad_nz;
     for (int k = 1; k <= K; ++k) {
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
-        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items, partials, h,
-                               y, d, d, ep, xdiv, s))
+        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items,
+                               partials, h, y, d, d, ep, xdiv, x_nz, s))
             return e;
         if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;
         h = dense_rows(y, n, d);
         xdiv = 1.f;
+        x_nz = nullptr;
     }
     return 0;
 }

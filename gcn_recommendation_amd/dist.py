@@ -36,7 +36,9 @@ def init(device_type="cuda", backend=None):
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    backend = backend or ("nccl" if device_type == "cuda" else "gloo")
+    # LGCN_DIST_BACKEND=gloo rehearses the multi-process GPU path on a one-GPU box
+    backend = backend or os.environ.get("LGCN_DIST_BACKEND") or (
+        "nccl" if device_type == "cuda" else "gloo")
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
@@ -340,6 +342,8 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
                      dtype=torch.float64, device=dev)
     tmax = t.clone()
+    if dist.get_backend() == "gloo":  # rehearsal on one GPU: reduce on the host
+        tmax = tmax.cpu()
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     ms_max, kern_ms, all_ms = (float(x) for x in tmax.tolist())
     value = K * nnz * args.steps / (ms_max / 1e3)

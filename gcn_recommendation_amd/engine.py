@@ -41,7 +41,7 @@ class EpilogueT(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("n_prev", ctypes.c_int32), ("div", ctypes.c_float),
                 ("pad", ctypes.c_int32), ("prev0", RowsT),
                 ("prev_dense", ctypes.c_void_p * LGCN_MAX_LAYERS), ("ld_prev", ctypes.c_int64),
-                ("addend", RowsT)]
+                ("addend", RowsT), ("addend_nz", ctypes.c_void_p)]
 
 
 class LgcnError(RuntimeError):
@@ -74,14 +74,15 @@ ABI = [
     ("lgcn_score_topk", ctypes.c_int, [_P, _I64, _P, _I32, _P, _I64, _I32, _I32, _P, _P, _I32,
                                        _I32, _P, _P, _P, _P, _P]),
     ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, RowsT, ctypes.c_float,
-                                       _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
+                                       _P, _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_rows_nonzero", ctypes.c_int, [RowsT, _I32, _I32, _P, _P, _P]),
     ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _P, _P, _I64, _I32,
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
     ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _P,
                                               RowsT, _I32, _I32, _P, _P, _P, _P]),
     ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _P,
-                                               RowsT, _I32, _I32, _P, _P, _P]),
+                                               RowsT, _P, _I32, _I32, _P, _P, _P]),
 ]
 
 
@@ -464,8 +465,10 @@ def _check_emb(segments, d, device):
             raise LgcnError("embedding blocks must be contiguous [rows x d]")
 
 
-def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0):
-    """One layer Y = epilogue(Â·(X / x_div)) through lgcn_spmm_layer + lgcn_hub_combine."""
+def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0,
+               x_nz=None):
+    """One layer Y = epilogue(Â·(X / x_div)) through lgcn_spmm_layer + lgcn_hub_combine.
+    x_nz: optional row bitmask of X (rows_nonzero; ADD epilogue only)."""
     lib = load_library()
     hp = hubs or graph.hubs(hub_threshold)
     partials = None
@@ -476,7 +479,7 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     _check(lib.lgcn_spmm_layer(_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids),
                                graph.n_rows,
                                min(hp.threshold, INT32_MAX), _ptr(hp.items), hp.n_items,
-                               _ptr(partials), x, x_div, _ptr(y), y.stride(0), d,
+                               _ptr(partials), x, x_div, _ptr(x_nz), _ptr(y), y.stride(0), d,
                                ctypes.byref(epi), stream), "lgcn_spmm_layer")
     if hp.n_rows:
         _check(lib.lgcn_hub_combine(_ptr(hp.rows), hp.n_rows, _ptr(partials), _ptr(y), y.stride(0),
@@ -527,12 +530,55 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
         return (out, layers) if return_layers else out
 
 
-def propagate_backward(graph, grad_out, K, hub_threshold=None):
+def rows_nonzero(segments, d, device):
+    """(bitmask of rows holding a nonzero, device int32 count of such rows): lgcn_rows_nonzero.
+    Nothing is read back."""
+    lib = load_library()
+    n = sum(int(t.shape[0]) for t in segments)
+    mask = torch.empty(max((n + 31) // 32, 1), dtype=torch.int32, device=device)
+    count = torch.empty(1, dtype=torch.int32, device=device)
+    with torch.cuda.device(device):
+        _check(lib.lgcn_rows_nonzero(rows_desc(segments, d), n, d, _ptr(mask), _ptr(count),
+                                     _stream(device)), "lgcn_rows_nonzero")
+    return mask, count
+
+
+def _live_fraction_sample(segments, n, samples=4096):
+    """Fraction of live (nonzero) rows among `samples` evenly spaced rows (one small sync):
+    decides whether the masked backward pays for its mask pass."""
+    idx = np.unique(np.linspace(0, n - 1, min(samples, n)).astype(np.int64))
+    parts, acc = [], 0
+    for t in segments:
+        sel = idx[(idx >= acc) & (idx < acc + t.shape[0])] - acc
+        if sel.size:
+            parts.append(t.index_select(0, torch.from_numpy(sel).to(t.device)))
+        acc += t.shape[0]
+    rows = torch.cat(parts, 0)
+    return float((rows != 0).any(1).float().mean().item())
+
+
+# Row-sparse backward: the upstream gradient of a BPR batch (main.py:496-497 gathers, then
+# IndexBackward scatters into zeros) has a few thousand live rows out of millions. Below this
+# live fraction the backward skips G's zero rows (bitwise-neutral); env LGCN_SPARSE_GRAD = auto
+# (default) | off | on.
+SPARSE_GRAD_MAX_FRAC = 0.25
+
+
+def _sparse_grad_mode():
+    m = os.environ.get("LGCN_SPARSE_GRAD", "auto").lower()
+    if m not in ("auto", "off", "on"):
+        raise LgcnError(f"LGCN_SPARSE_GRAD={m!r} (auto | off | on)")
+    return m
+
+
+def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None):
     """dE0 = Σ_k (Âᵀ)^k G/(K+1), Horner order h = G/(K+1) + Âᵀ h (autograd's accumulation).
 
     grad_out: the [n x d] upstream gradient, or a list of row blocks (the user / item / brand
     output gradients, read in place). c = G/(K+1) is never materialised: layer 1 divides on
-    load and every epilogue adds G[row]/(K+1) — the same rounding as a stored c."""
+    load and every epilogue adds G[row]/(K+1) — the same rounding as a stored c.
+    sparse: "auto" | "off" | "on" (default: env LGCN_SPARSE_GRAD): with a row-sparse G, layer 1
+    gathers only G's live rows and the epilogues skip its zero rows — same bits, fewer bytes."""
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
     gt = graph.transpose
@@ -551,13 +597,19 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None):
             _check(lib.lgcn_scale_rows(g, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
             return out
         hp = gt.hubs(hub_threshold)
+        mode = sparse or _sparse_grad_mode()
+        nz = None
+        if mode == "on" or (mode == "auto" and n > 0 and
+                            _live_fraction_sample(segs, n) <= SPARSE_GRAD_MAX_FRAC):
+            nz, _ = rows_nonzero(segs, d, dev)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
         ep = _epilogue(LGCN_EPI_ADD, addend=g, div=float(K + 1))
+        ep.addend_nz = None if nz is None else nz.data_ptr()
         h = segs
         for k in range(1, K + 1):
             y = out if (K - k) % 2 == 0 else work
             spmm_layer(gt, h, y, d, ep, hub_threshold, hp, stream,
-                       x_div=float(K + 1) if k == 1 else 1.0)
+                       x_div=float(K + 1) if k == 1 else 1.0, x_nz=nz if k == 1 else None)
             h = [y]
         return out
 

@@ -93,7 +93,9 @@ typedef struct {
 
 /* Epilogue operands. MEAN: prev0 is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
  * dense layer buffers E1..E_{n_prev-1} with leading dimension ld_prev, div = K+1. ADD: addend
- * is a segmented block Z, div its divisor (1 = plain add; the backward passes G and K+1). */
+ * is a segmented block Z, div its divisor (1 = plain add; the backward passes G and K+1);
+ * addend_nz: NULL, or a row bitmask (lgcn_rows_nonzero) — rows whose bit is 0 are all zero and
+ * are not read (results unchanged). */
 typedef struct {
     int32_t mode;
     int32_t n_prev;
@@ -103,6 +105,7 @@ typedef struct {
     const float* prev_dense[LGCN_MAX_LAYERS];
     int64_t ld_prev;
     lgcn_rows_t addend;
+    const uint32_t* addend_nz;
 } lgcn_epilogue_t;
 
 /* ---- identification ---------------------------------------------------------------------- */
@@ -194,16 +197,24 @@ int lgcn_adj_finish(const uint64_t* uniq, const int32_t* counts, int64_t nnz, in
  * X is read through `x` (segments allowed); x_div = 1 reads it as is, otherwise every gathered
  * element is divided by x_div once (ADD epilogue only: the backward's G/(K+1)).
  * Y is [n_rows x ldy]. d in [1, 2048]. row_ids: NULL, or the slot -> row map of a
- * degree-ordered CSR (see Conventions). */
+ * degree-ordered CSR (see Conventions). x_nz (ADD epilogue only): NULL, or the row bitmask of
+ * X from lgcn_rows_nonzero — edges into all-zero rows of X are skipped, bitwise-neutrally (a
+ * row-sparse upstream gradient makes the first backward layer read only its live rows). */
 int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
-                    int32_t n_rows, int32_t hub_threshold, const lgcn_hub_item_t* hub_items, int32_t n_hub_items,
-                    float* partials, lgcn_rows_t x, float x_div, float* y, int64_t ldy, int32_t d,
+                    int32_t n_rows, int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
+                    int32_t n_hub_items, float* partials, lgcn_rows_t x, float x_div,
+                    const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
                     const lgcn_epilogue_t* epi_host, void* stream);
 
 /* Finish hub rows: sum each row's partial slots in slot order, apply the epilogue, write Y. */
 int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
                      float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
                      void* stream);
+
+/* Row-sparsity of a block: mask[(n_rows+31)/32] gets bit r set iff row r holds a value != 0
+ * (NaN included); *count (device int32) = number of such rows. No pre-zeroing needed. */
+int lgcn_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t d, uint32_t* mask, int32_t* count,
+                      void* stream);
 
 /* Y[r,:] = X[r,:] / div for r < n_rows (mean of one layer; backward seed G/(K+1)). */
 int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
@@ -224,13 +235,16 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
 /* Whole backward: grad_e0 = sum_k (Âᵀ)^k G/(K+1) in the Horner order autograd uses
  * (c = G/(K+1); h = c; K times h = c + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric).
  * G is read in place as segments (the user/item/brand output grads); c is never stored.
+ * grad_nz: NULL, or G's row bitmask (lgcn_rows_nonzero): a BPR batch touches a few thousand
+ * rows, so the first layer gathers only those and no epilogue reads G's zero rows.
  * work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. */
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const int32_t* row_ids, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out, int32_t d,
-                            int32_t K, float* work_h, float* grad_e0, void* stream);
+                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out,
+                            const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
+                            float* grad_e0, void* stream);
 
 /* ---- evaluation (main.py:404-439) ----------------------------------------------------------- */
 /* Item splits for lgcn_score_topk: ~2 blocks per CU, >= 2048 items per split, <= 256. */

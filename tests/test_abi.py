@@ -53,19 +53,21 @@ def test_argument_validation_without_gpu(lib):
     ep.mode = 7
     rows = engine.RowsT()
     # bad epilogue / bad d / negative sizes return before any HIP call
-    assert lib.lgcn_spmm_layer(None, None, None, 0, 0, None, 0, None, rows, 1.0, None, 0, 64,
-                               ctypes.byref(ep), None) == -1
+    assert lib.lgcn_spmm_layer(None, None, None, 0, 0, None, 0, None, rows, 1.0, None, None, 0,
+                               64, ctypes.byref(ep), None) == -1
     ep.mode = engine.LGCN_EPI_STORE
-    assert lib.lgcn_spmm_layer(None, None, None, 10, 0, None, 0, None, rows, 1.0, None, 0, 0,
-                               ctypes.byref(ep), None) == -1
-    assert lib.lgcn_spmm_layer(None, None, None, -1, 0, None, 0, None, rows, 1.0, None, 0, 64,
-                               ctypes.byref(ep), None) == -1
-    assert lib.lgcn_spmm_layer(None, None, None, 0, 0, None, 0, None, rows, 0.0, None, 64, 64,
-                               ctypes.byref(ep), None) == -1
+    assert lib.lgcn_spmm_layer(None, None, None, 10, 0, None, 0, None, rows, 1.0, None, None, 0,
+                               0, ctypes.byref(ep), None) == -1
+    assert lib.lgcn_spmm_layer(None, None, None, -1, 0, None, 0, None, rows, 1.0, None, None, 0,
+                               64, ctypes.byref(ep), None) == -1
+    assert lib.lgcn_spmm_layer(None, None, None, 0, 0, None, 0, None, rows, 0.0, None, None, 64,
+                               64, ctypes.byref(ep), None) == -1
     ep.mode = engine.LGCN_EPI_MEAN
     ep.n_prev = 18
     ep.div = 2.0
     assert lib.lgcn_hub_combine(None, 0, None, None, 64, 64, ctypes.byref(ep), None) == -3
+    assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 64, None, None, None) == -1
+    assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 0, None, None, None) == -1
     assert lib.lgcn_propagate_forward(None, None, None, 5, 0, None, 0, None, 0, None, rows, 64, -1,
                                       None, None, None, None) == -1
     nbytes = ctypes.c_size_t(0)
@@ -86,9 +88,9 @@ def test_struct_layout_matches_header():
 int main(void){
  printf("%zu %zu %zu %zu\n", sizeof(lgcn_rows_t), sizeof(lgcn_epilogue_t),
         sizeof(lgcn_hub_item_t), sizeof(lgcn_hub_row_t));
- printf("%zu %zu %zu %zu\n", offsetof(lgcn_epilogue_t, prev0),
+ printf("%zu %zu %zu %zu %zu\n", offsetof(lgcn_epilogue_t, prev0),
         offsetof(lgcn_epilogue_t, prev_dense), offsetof(lgcn_epilogue_t, ld_prev),
-        offsetof(lgcn_epilogue_t, addend));
+        offsetof(lgcn_epilogue_t, addend), offsetof(lgcn_epilogue_t, addend_nz));
  return 0;}
 """
     with tempfile.TemporaryDirectory() as td:
@@ -101,7 +103,8 @@ int main(void){
     offs = [int(x) for x in l2.split()]
     assert sizes == [ctypes.sizeof(engine.RowsT), ctypes.sizeof(engine.EpilogueT), 16, 16]
     E = engine.EpilogueT
-    assert offs == [E.prev0.offset, E.prev_dense.offset, E.ld_prev.offset, E.addend.offset]
+    assert offs == [E.prev0.offset, E.prev_dense.offset, E.ld_prev.offset, E.addend.offset,
+                    E.addend_nz.offset]
 
 
 def test_engine_refuses_missing_library(tmp_path):

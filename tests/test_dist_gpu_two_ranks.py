@@ -51,6 +51,10 @@ def _worker(rank, world, port, q):
         sl, (c0, c1) = D.featsplit_slices(segs, world, rank)
         mine = D.featsplit_forward(g, sl, K, engine.INT32_MAX).cpu()
         out["featsplit"] = bool(np.array_equal(mine.numpy(), want[:, c0:c1]))
+        fs = D.FeatSplitPlan(rowptr, c, v, n, dev)      # slot-space shards (bench.py's path)
+        x, (c0, c1) = fs.shard(segs, world, rank)
+        mine = fs.unshard(fs.forward(x, K, engine.INT32_MAX)).cpu()
+        out["featsplit"] &= bool(np.array_equal(mine.numpy(), want[:, c0:c1]))
         D.shutdown()
         q.put((rank, out))
     except Exception:
