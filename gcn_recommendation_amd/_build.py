@@ -6,7 +6,7 @@ import subprocess
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
-SRCS = [os.path.join(_PKG, "csrc", f) for f in ("lgcn_engine.hip", "lgcn_eval.hip")]
+SRCS = [os.path.join(_PKG, "csrc", f) for f in ("lgcn_engine.hip", "lgcn_eval.hip", "lgcn_bpr.hip")]
 HDR = os.path.join(ROOT, "include", "lgcn.h")
 OUT = os.path.join(_PKG, "liblgcn_engine.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]

@@ -246,6 +246,17 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                             float* grad_e0, void* stream);
 
+/* ---- training batch loss (main.py:366-402) -------------------------------------------------- */
+/* Fused BPR + L2 loss of one batch of B gathered rows (u, p, n = final user / positive /
+ * negative item rows; u0, p0, n0 = their layer-0 rows; row-major, leading dims ld*):
+ *   *loss = -mean_b log(sigmoid(<u_b,p_b> - <u_b,n_b>) + 1e-8) + lambda*(|U0|^2+|P0|^2+|N0|^2)/B
+ * and d(loss)/d(input) for all six inputs into grads = [6 x B x d] (order u, p, n, u0, p0, n0,
+ * each dense [B x d]). terms: scratch [2 x B]. The batch reduction runs in a fixed order. */
+int lgcn_bpr_loss(const float* u, int64_t ldu, const float* p, int64_t ldp, const float* n,
+                  int64_t ldn, const float* u0, int64_t ldu0, const float* p0, int64_t ldp0,
+                  const float* n0, int64_t ldn0, int32_t B, int32_t d, float lambda, float* terms,
+                  float* loss, float* grads, void* stream);
+
 /* ---- evaluation (main.py:404-439) ----------------------------------------------------------- */
 /* Item splits for lgcn_score_topk: ~2 blocks per CU, >= 2048 items per split, <= 256. */
 int lgcn_eval_splits(int32_t n_users, int32_t n_items, int32_t n_cu);
