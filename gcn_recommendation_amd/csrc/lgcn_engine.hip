@@ -1,7 +1,7 @@
 // lgcn_engine.hip — MI355X (gfx950, CDNA4) kernels + C ABI for LightGCN propagation.
 //
 // Replaces, for a HIP device, the reference hot path (models/lightgcn.py:37-59 and
-// models/lightgcn_fusion.py:132-142): E_{k+1} = Â·E_k for K layers (torch.sparse.mm, lightgcn.py:45),
+// models/lightgcn_fusion.py:52-59): E_{k+1} = Â·E_k for K layers (torch.sparse.mm, lightgcn.py:45),
 // the layer mean (lightgcn.py:54), and the autograd backward of both. Declarations and the
 // numerics contract: include/lgcn.h. Design and byte model: DESIGN.md.
 //

@@ -5,7 +5,7 @@
  *     ego = cat(user, item, brand)                         models/lightgcn.py:37-40
  *     for k < K: ego = torch.sparse.mm(adj_mat, ego)       models/lightgcn.py:44-46
  *     final = mean(stack([E0..EK]), 0)                     models/lightgcn.py:54
- *     (and the identical loop, models/lightgcn_fusion.py:132-139)
+ *     (and the identical loop, models/lightgcn_fusion.py:52-59)
  * plus its autograd backward (torch SparseAddmmBackward0 + MeanBackward + CatBackward), and the
  * one-time conversion of the caller-owned `torch.sparse_coo_tensor` Â (main.py:331-336) into the
  * engine's CSR form. A ctypes binding of every entry point ships in

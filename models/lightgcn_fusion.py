@@ -1,4 +1,4 @@
-"""Drop-in `models.lightgcn_fusion.LightGCN_Fusion` (reference models/lightgcn_fusion.py:5-65).
+"""Drop-in `models.lightgcn_fusion.LightGCN_Fusion` (reference models/lightgcn_fusion.py:5-64).
 
 Same constructor (raises without pretrained content embeddings), module registration and RNG
 order (user, item_id, brand embeddings, fusion Linear, then four xavier inits), buffer

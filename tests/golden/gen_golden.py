@@ -2,7 +2,7 @@
 
 This script is the only place that touches `/root/reference`. It imports the reference's own
 `main.load_preprocessed_data` (main.py:172-347), `models.lightgcn.LightGCN` (lightgcn.py:4-81),
-`models.lightgcn_fusion.LightGCN_Fusion` (lightgcn_fusion.py:5-65), `main.bpr_loss_reg`
+`models.lightgcn_fusion.LightGCN_Fusion` (lightgcn_fusion.py:5-64), `main.bpr_loss_reg`
 (main.py:366-402) and `main.evaluate` (main.py:404-439), runs them on CPU on small seeded synthetic
 graphs, and dumps inputs + outputs as `.npz` data fixtures next to this file. Only data leaves the
 reference: edge lists, the normalised adjacency it built, embeddings, gradients, losses, metrics.
