@@ -1,15 +1,23 @@
 """Build liblgcn_engine.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with
-the repo snapshot to the GPU box)."""
+the repo snapshot to the GPU box). Each .hip translation unit compiles to an object in
+parallel (the k_layer instantiations are split by epilogue mode), then one link."""
 import os
 import shutil
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
-SRCS = [os.path.join(_PKG, "csrc", f) for f in ("lgcn_engine.hip", "lgcn_eval.hip", "lgcn_bpr.hip")]
-HDR = os.path.join(ROOT, "include", "lgcn.h")
+CSRC = os.path.join(_PKG, "csrc")
+SRCS = [os.path.join(CSRC, f) for f in (
+    "lgcn_layer_add_sparse.hip", "lgcn_layer_add_div.hip", "lgcn_layer_add.hip",
+    "lgcn_layer_mean.hip", "lgcn_layer_store.hip", "lgcn_engine.hip", "lgcn_eval.hip",
+    "lgcn_bpr.hip")]
+HDRS = [os.path.join(ROOT, "include", "lgcn.h"), os.path.join(CSRC, "lgcn_kernels.h")]
 OUT = os.path.join(_PKG, "liblgcn_engine.so")
+OBJ_DIR = os.path.join(_PKG, "_obj")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 
 
 def hipcc():
@@ -23,17 +31,30 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in SRCS + [HDR, __file__])
+    return any(os.path.getmtime(p) > t for p in SRCS + HDRS + [__file__])
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, jobs=None):
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-I", os.path.join(ROOT, "include")] + SRCS + \
-          ["-o", OUT + ".tmp"]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    cc = hipcc()
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", CSRC]
+
+    def compile_one(src):
+        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        cmd = [cc] + FLAGS + inc + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        return obj
+
+    n = jobs or min(len(SRCS), max(1, min(8, (os.cpu_count() or 2))))
+    with ThreadPoolExecutor(n) as pool:
+        objs = list(pool.map(compile_one, SRCS))
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", OUT + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(OUT + ".tmp", OUT)
     return OUT
