@@ -175,8 +175,8 @@ def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
     nnz = adj._nnz()
     out = {"ms_per_step": round(ms, 3), "propagated_edges_per_s": round(2 * K * nnz / (ms / 1e3), 1),
            "batch": 2048, "optimizer": "Adam(lr=1e-3)", "loss_last": float(loss.item()),
-           "what": "main.py:488-531 hot loop: forward + gathers + bpr_loss_reg + backward + "
-                   "Adam over all 14.7M x 64 parameters"}
+           "what": f"main.py:488-531 hot loop: forward + gathers + bpr_loss_reg + backward + "
+                   f"Adam over all {U + I:,} x {d} parameters"}
     del model, opt
     torch.cuda.empty_cache()
     return out
