@@ -43,6 +43,9 @@ def build(force=False, verbose=False, jobs=None):
 
     def compile_one(src):
         obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        if not force and os.path.exists(obj) and all(
+                os.path.getmtime(obj) > os.path.getmtime(p) for p in [src] + HDRS + [__file__]):
+            return obj  # up to date (incremental rebuild)
         cmd = [cc] + FLAGS + inc + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
