@@ -506,3 +506,22 @@ def test_fused_bpr_loss_vs_torch(gpu_device, d):
     assert abs(got - want) <= 1e-6 * abs(want), (got, want)
     for a, b in zip(g_got, g_want):
         assert_close_normwise(a, b, what="bpr grad")
+
+
+def test_captured_forward_hipgraph(gpu_device):
+    """engine.CapturedForward: the forward recorded into a HIP graph replays bitwise the eager
+    result, and sees in-place updates of its input buffers (an optimizer step)."""
+    z = load_case("c1_brand")
+    U, I, B, d, K = case_dims(z)
+    adj = _adj(z, gpu_device)
+    g = engine.graph_from_coo(adj)
+    segs = [torch.from_numpy(z[f"param/{k}_embedding.weight"]).to(gpu_device)
+            for k in ("user", "item", "brand")]
+    cap = engine.CapturedForward(g, segs, K)
+    got = cap.replay().cpu().numpy()
+    assert np.array_equal(got, oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"],
+                                              case_e0(z), K))
+    for t in segs:
+        t.mul_(0.5)
+    again = cap.replay()
+    assert torch.equal(again, engine.propagate_forward(g, segs, K))
