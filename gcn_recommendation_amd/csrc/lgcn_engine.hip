@@ -112,6 +112,44 @@ __global__ void k_csr_degrees(const int32_t* __restrict__ rowptr, int32_t n,
     iota[r] = (int32_t)r;
 }
 
+// rank[row_ids[s]] = s: position of every row in the degree-descending order
+__global__ void k_csr_rank(const int32_t* __restrict__ row_ids, int32_t n, int32_t* __restrict__ rank) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    rank[row_ids[s]] = (int32_t)s;
+}
+
+// Tie-break key of the slot order: among rows of equal degree, rows whose least popular
+// neighbour (highest degree rank) is the same sit next to each other, so a neighbour's row
+// gathers them from consecutive slots (several rows of a narrow shard per 128-B line).
+// comp = deg << 32 | ~(key + 1), sorted descending: degree descending, then key ascending;
+// rows above kKeyMaxDeg (hubs: their degrees rarely tie) and empty rows get key 0.
+constexpr int32_t kKeyMaxDeg = 256;
+__global__ void k_csr_degree_key(const int32_t* __restrict__ rowptr,
+                                 const lgcn_edge_t* __restrict__ edges, int32_t n,
+                                 const int32_t* __restrict__ rank, uint64_t* __restrict__ comp,
+                                 int32_t* __restrict__ iota) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int32_t b = rowptr[r], e = rowptr[r + 1];
+    uint32_t key = 0;
+    if (e - b <= kKeyMaxDeg)
+        for (int32_t j = b; j < e; ++j) {
+            const uint32_t k = (uint32_t)rank[(int32_t)edges[j]] + 1u;
+            key = k > key ? k : key;
+        }
+    comp[r] = ((uint64_t)(uint32_t)(e - b) << 32) | (uint64_t)(0xFFFFFFFFu - key);
+    iota[r] = (int32_t)r;
+}
+
+__global__ void k_csr_slot_degrees(const int32_t* __restrict__ row_ids,
+                                   const int32_t* __restrict__ deg, int32_t n,
+                                   int32_t* __restrict__ deg_sorted) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    deg_sorted[s] = deg[row_ids[s]];
+}
+
 // edges_out[j] = the edge record of slot s (binary search: rowptr_out[s] <= j < rowptr_out[s+1])
 __global__ void k_csr_gather_rows(const int32_t* __restrict__ rowptr_out,
                                   const int32_t* __restrict__ row_ids,
@@ -402,34 +440,59 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
 int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
                              int64_t nnz, int32_t* deg_tmp, int32_t* deg_sorted, int32_t* iota_tmp,
                              int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
+                             uint64_t* key_tmp, uint64_t* key_sorted,
                              void* temp, size_t* temp_bytes_host, void* stream) {
     if (n_rows < 0 || nnz < 0 || nnz > 0x7fffffffLL || !temp_bytes_host) return LGCN_EINVAL;
+    if ((key_tmp == nullptr) != (key_sorted == nullptr)) return LGCN_EINVAL;
     int end_bit = 1;  // degrees are <= nnz
     while (end_bit < 31 && (1LL << end_bit) <= nnz) ++end_bit;
     hipStream_t s = S(stream);
     const int n = n_rows;
+    const bool keyed = key_tmp != nullptr;
     if (temp == nullptr) {
-        size_t b1 = 0, b2 = 0;
+        size_t b1 = 0, b2 = 0, b3 = 0;
         hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(
             nullptr, b1, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, end_bit, s);
         if (e != hipSuccess) return (int)e;
         e = hipcub::DeviceScan::InclusiveSum(nullptr, b2, deg_sorted, rowptr_out, n, s);
-        *temp_bytes_host = b1 > b2 ? b1 : b2;
-        return herr(e);
+        if (e != hipSuccess) return (int)e;
+        if (keyed) {
+            e = hipcub::DeviceRadixSort::SortPairsDescending(
+                nullptr, b3, key_tmp, key_sorted, iota_tmp, row_ids, n, 0, 32 + end_bit, s);
+            if (e != hipSuccess) return (int)e;
+        }
+        size_t b = b1 > b2 ? b1 : b2;
+        *temp_bytes_host = b > b3 ? b : b3;
+        return 0;
     }
     if (!rowptr || !rowptr_out || (n > 0 && (!deg_tmp || !deg_sorted || !iota_tmp || !row_ids)))
         return LGCN_EINVAL;
     if (nnz > 0 && (!edges || !edges_out)) return LGCN_EINVAL;
     if (int e = herr(hipMemsetAsync(rowptr_out, 0, sizeof(int32_t), s))) return e;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_csr_degrees, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       s, rowptr, n, deg_tmp, iota_tmp);
+    const dim3 gn((uint32_t)((n + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(k_csr_degrees, gn, dim3(kBlock), 0, s, rowptr, n, deg_tmp, iota_tmp);
     if (int e = last_err()) return e;
     size_t bytes = *temp_bytes_host;
     // LSD radix sort: stable, so rows of equal degree keep their id order
     if (int e = herr(hipcub::DeviceRadixSort::SortPairsDescending(
             temp, bytes, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, end_bit, s)))
         return e;
+    if (keyed) {  // second, stable sort by (degree, neighbour key); the permutation only
+        // reorders work and slots, every row keeps its edges (bitwise-neutral)
+        hipLaunchKernelGGL(k_csr_rank, gn, dim3(kBlock), 0, s, row_ids, n, deg_sorted);
+        if (int e = last_err()) return e;
+        hipLaunchKernelGGL(k_csr_degree_key, gn, dim3(kBlock), 0, s, rowptr, edges, n, deg_sorted,
+                           key_tmp, iota_tmp);
+        if (int e = last_err()) return e;
+        bytes = *temp_bytes_host;
+        if (int e = herr(hipcub::DeviceRadixSort::SortPairsDescending(
+                temp, bytes, key_tmp, key_sorted, iota_tmp, row_ids, n, 0, 32 + end_bit, s)))
+            return e;
+        hipLaunchKernelGGL(k_csr_slot_degrees, gn, dim3(kBlock), 0, s, row_ids, deg_tmp, n,
+                           deg_sorted);
+        if (int e = last_err()) return e;
+    }
     bytes = *temp_bytes_host;
     if (int e = herr(hipcub::DeviceScan::InclusiveSum(temp, bytes, deg_sorted, rowptr_out + 1, n, s)))
         return e;

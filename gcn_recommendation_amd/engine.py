@@ -24,7 +24,7 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL = 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
@@ -64,7 +64,7 @@ ABI = [
                                           ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
     ("lgcn_csr_order_by_degree", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P,
-                                                ctypes.POINTER(ctypes.c_size_t), _P]),
+                                                _P, _P, ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_csr_relabel_cols", ctypes.c_int, [_P, _I64, _P, _P, _P]),
     ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),  # (sorted keys, ...)
     ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
@@ -279,24 +279,36 @@ class Graph:
         return out
 
 
+def slot_key_enabled(g):
+    """Neighbour-key tie-break of the slot order (square operators; env LGCN_SLOT_KEY=0 turns it
+    off): rows of equal degree grouped by their least popular neighbour."""
+    return g.n_rows == g.n_cols and os.environ.get("LGCN_SLOT_KEY", "1") != "0"
+
+
 def order_by_degree(lib, g, stream):
     """The same operator with its rows stored in degree-descending slots (lgcn_csr_order_by_degree):
-    lane groups of a wave then stream rows of equal length. Bitwise-neutral."""
+    lane groups of a wave then stream rows of equal length; ties grouped by neighbour key
+    (slot_key_enabled). Bitwise-neutral."""
     n, nnz, dev = g.n_rows, g.nnz, g.device
     i32 = dict(dtype=torch.int32, device=dev)
     deg_tmp, deg_sorted, iota = (torch.empty(max(n, 1), **i32) for _ in range(3))
     row_ids = torch.empty(max(n, 1), **i32)
     rowptr = torch.empty(n + 1, **i32)
     edges = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+    keys = (torch.empty(max(n, 1), dtype=torch.int64, device=dev) for _ in range(2)) \
+        if slot_key_enabled(g) else (None, None)
+    key_tmp, key_sorted = keys
     nbytes = ctypes.c_size_t(0)
     args = (_ptr(g.rowptr), _ptr(g.edges), n, nnz, _ptr(deg_tmp), _ptr(deg_sorted), _ptr(iota),
-            _ptr(row_ids), _ptr(rowptr), _ptr(edges))
+            _ptr(row_ids), _ptr(rowptr), _ptr(edges),
+            _ptr(key_tmp) if key_tmp is not None else None,
+            _ptr(key_sorted) if key_sorted is not None else None)
     _check(lib.lgcn_csr_order_by_degree(*args, None, ctypes.byref(nbytes), stream),
            "lgcn_csr_order_by_degree(size)")
     temp = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
     _check(lib.lgcn_csr_order_by_degree(*args, _ptr(temp), ctypes.byref(nbytes), stream),
            "lgcn_csr_order_by_degree")
-    del deg_tmp, deg_sorted, iota, temp
+    del deg_tmp, deg_sorted, iota, temp, key_tmp, key_sorted
     o = Graph(n, g.n_cols, rowptr, edges, nnz, dev, row_ids=row_ids[:n])
     o.symmetric = g.symmetric
     return o

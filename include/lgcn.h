@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 2
+#define LGCN_ABI_VERSION 3
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -150,13 +150,18 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
                              int64_t nnz, int32_t* asym, void* stream);
 
 /* Degree-ordered copy of a CSR for the propagation kernels: row_ids[s] = the row processed in
- * slot s (degree descending, ties in row order: a stable radix sort), rowptr_out[n_rows+1] /
- * edges_out[nnz] = the rows in slot order, each row's edges in their original order (so every
- * result is bitwise unchanged). Scratch deg_tmp / deg_sorted / iota_tmp: n_rows int32 each.
- * Two-call protocol for temp (temp == NULL: only *temp_bytes_host is written). */
+ * slot s (degree descending), rowptr_out[n_rows+1] / edges_out[nnz] = the rows in slot order,
+ * each row's edges in their original order (so every result is bitwise unchanged). Ties: with
+ * key_tmp / key_sorted NULL, row order (a stable radix sort); with them (n_rows uint64 each,
+ * square operators only: columns index rows), rows of equal degree are grouped by their least
+ * popular neighbour (highest degree rank) — rows gathered by the same row then sit in
+ * consecutive slots, which a narrow (featsplit) shard turns into shared 128-B lines.
+ * Scratch deg_tmp / deg_sorted / iota_tmp: n_rows int32 each. Two-call protocol for temp
+ * (temp == NULL: only *temp_bytes_host is written; pass the same key pointers both times). */
 int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
                              int64_t nnz, int32_t* deg_tmp, int32_t* deg_sorted, int32_t* iota_tmp,
                              int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
+                             uint64_t* key_tmp, uint64_t* key_sorted,
                              void* temp, size_t* temp_bytes_host, void* stream);
 
 /* Column relabelling: edges_out[j] = edges[j] with column c replaced by new_id[c]. With the

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 2
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 3
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -74,9 +74,14 @@ def test_argument_validation_without_gpu(lib):
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
                                   ctypes.byref(nbytes), None) == -1
     assert lib.lgcn_csr_order_by_degree(None, None, -1, 0, None, None, None, None, None, None,
-                                        None, ctypes.byref(nbytes), None) == -1
+                                        None, None, None, ctypes.byref(nbytes), None) == -1
     assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, None, None, None, None, None, None,
-                                        ctypes.c_void_p(1), ctypes.byref(nbytes), None) == -1
+                                        None, None, ctypes.c_void_p(1), ctypes.byref(nbytes),
+                                        None) == -1
+    # the two key buffers come together or not at all
+    assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, None, None, None, None, None, None,
+                                        ctypes.c_void_p(8), None, None, ctypes.byref(nbytes),
+                                        None) == -1
 
 
 def test_struct_layout_matches_header():

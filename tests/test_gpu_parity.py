@@ -258,10 +258,29 @@ def test_hub_rows_chunked_vs_exact(gpu_device, order):
     assert g.hubs(256).n_rows >= 1
 
 
-def test_degree_order_plan(gpu_device):
+def expected_slot_order(rp, cols, keyed=True):
+    """Restatement of lgcn_csr_order_by_degree's slot order: degree descending; ties (keyed) by
+    the highest degree rank among the row's neighbours + 1 (0 for empty rows and rows above 256
+    edges), then row id."""
+    n = rp.size - 1
+    deg = np.diff(rp)
+    if not keyed:
+        return np.lexsort((np.arange(n), -deg))
+    rank0 = np.empty(n, np.int64)
+    rank0[np.lexsort((np.arange(n), -deg))] = np.arange(n)
+    key = np.zeros(n, np.int64)
+    for r in range(n):
+        if 0 < deg[r] <= 256:
+            key[r] = rank0[cols[rp[r]:rp[r + 1]]].max() + 1
+    return np.lexsort((np.arange(n), key, -deg))
+
+
+@pytest.mark.parametrize("keyed", [True, False])
+def test_degree_order_plan(gpu_device, monkeypatch, keyed):
     """lgcn_csr_order_by_degree: row_ids is a permutation, slots hold degrees in descending order
-    with ties in row-id order (stable), each slot's edges are its row's edges in stored order,
-    and the hub plan's output rows are row ids."""
+    with ties grouped by neighbour key (or, unkeyed, in row-id order), each slot's edges are its
+    row's edges in stored order, and the hub plan's output rows are row ids."""
+    monkeypatch.setenv("LGCN_SLOT_KEY", "1" if keyed else "0")
     z = load_case("hub_d32")
     adj = _adj(z, gpu_device)
     g = engine.graph_from_coo(adj)
@@ -275,7 +294,7 @@ def test_degree_order_plan(gpu_device):
     rp = np.searchsorted(r, np.arange(n + 1))
     deg = np.diff(rp)
     assert np.array_equal(deg_s, deg[ids])
-    assert np.array_equal(ids, np.lexsort((np.arange(n), -deg)))
+    assert np.array_equal(ids, expected_slot_order(rp, z["adj_col"].astype(np.int64), keyed))
     e = g.edges.cpu().numpy()
     want = engine.pack_edges(z["adj_col"], z["adj_val"])
     for s in np.random.default_rng(0).choice(n, 50, replace=False):
