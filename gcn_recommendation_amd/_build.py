@@ -34,19 +34,25 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in SRCS + HDRS + [__file__])
 
 
-def build(force=False, verbose=False, jobs=None):
-    if not force and not needs_build():
+def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
+    """variant: build an A/B copy (extra -D defines) as _variants/liblgcn_<variant>.so, loaded by
+    engine.load_library when LGCN_LIB points at it; the product library is untouched."""
+    out, obj_dir, flags = OUT, OBJ_DIR, FLAGS + [f"-D{d}" for d in defines]
+    if variant:
+        out = os.path.join(_PKG, "_variants", f"liblgcn_{variant}.so")
+        obj_dir = os.path.join(_PKG, "_variants", variant)
+    elif not force and not needs_build():
         return OUT
-    os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(obj_dir, exist_ok=True)
     cc = hipcc()
     inc = ["-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
     def compile_one(src):
-        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         if not force and os.path.exists(obj) and all(
                 os.path.getmtime(obj) > os.path.getmtime(p) for p in [src] + HDRS + [__file__]):
             return obj  # up to date (incremental rebuild)
-        cmd = [cc] + FLAGS + inc + ["-c", src, "-o", obj]
+        cmd = [cc] + flags + inc + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
@@ -55,13 +61,18 @@ def build(force=False, verbose=False, jobs=None):
     n = jobs or min(len(SRCS), max(1, min(8, (os.cpu_count() or 2))))
     with ThreadPoolExecutor(n) as pool:
         objs = list(pool.map(compile_one, SRCS))
-    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", OUT + ".tmp"]
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    # python -m gcn_recommendation_amd._build [variant DEFINE=VALUE ...]
+    import sys
+    if len(sys.argv) > 1:
+        print(build(variant=sys.argv[1], defines=sys.argv[2:], verbose=False))
+    else:
+        print(build(force=True, verbose=True))

@@ -87,8 +87,44 @@ __device__ __forceinline__ const float* seg_row(const lgcn_rows_t& s, int32_t r)
     return s.p2 + (int64_t)(r - s.end1) * s.ld;
 }
 
+// Streams touched once per layer (edge records, output rows, the mean epilogue's row reads) can
+// be marked non-temporal so they do not displace the gathered rows in L2 (LGCN_NT build flag).
+#ifndef LGCN_NT
+#define LGCN_NT 0
+#endif
+typedef float f4_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ int2 load_edge(const lgcn_edge_t* e) {
-    return *reinterpret_cast<const int2*>(e);
+    if constexpr (LGCN_NT & 1) {
+        const long long v = __builtin_nontemporal_load(reinterpret_cast<const long long*>(e));
+        return make_int2((int)(v & 0xffffffffLL), (int)(v >> 32));
+    } else {
+        return *reinterpret_cast<const int2*>(e);
+    }
+}
+
+template <typename V>
+__device__ __forceinline__ void store_out(float* p, V v) {
+    if constexpr ((LGCN_NT & 2) && VT<V>::W == 4) {
+        f4_t t = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(t, reinterpret_cast<f4_t*>(p));
+    } else if constexpr (LGCN_NT & 2) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        VT<V>::store(p, v);
+    }
+}
+
+template <typename V>
+__device__ __forceinline__ V load_stream(const float* p) {
+    if constexpr ((LGCN_NT & 4) && VT<V>::W == 4) {
+        const f4_t t = __builtin_nontemporal_load(reinterpret_cast<const f4_t*>(p));
+        return make_float4(t.x, t.y, t.z, t.w);
+    } else if constexpr (LGCN_NT & 4) {
+        return __builtin_nontemporal_load(p);
+    } else {
+        return VT<V>::load(p);
+    }
 }
 
 // Sequential fmaf chain over edge records [beg, end) — the ATen CPU order (one row's nonzeros in
@@ -182,9 +218,9 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
         V out = acc[q];
         if constexpr (MODE == LGCN_EPI_MEAN) {
             // ((E0 + E1) + ... + E_{K-1}) + E_K, then / (K+1): torch.mean(torch.stack(.), 0)
-            V s = T::load(seg_row(ep.prev0, row) + c * T::W);
+            V s = load_stream<V>(seg_row(ep.prev0, row) + c * T::W);
             for (int i = 0; i + 1 < ep.n_prev; ++i)
-                s = T::add(s, T::load(ep.prev_dense[i] + (int64_t)row * ep.ld_prev + c * T::W));
+                s = T::add(s, load_stream<V>(ep.prev_dense[i] + (int64_t)row * ep.ld_prev + c * T::W));
             s = T::add(s, out);
             out = div_exact<V>(s, ep.div, ep.pad);
         } else if constexpr (MODE == LGCN_EPI_ADD) {
@@ -194,7 +230,7 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
                 out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div,
                                           ep.pad), out);
         }
-        T::store(yr + c * T::W, out);
+        store_out<V>(yr + c * T::W, out);
     }
 }
 
@@ -325,7 +361,7 @@ __device__ __forceinline__ void mean_prefetch(const lgcn_epilogue_t& ep, int32_t
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int c = lane + q * G;
-            pre[p][q] = c < dW ? T::load(src + c * T::W) : T::zero();
+            pre[p][q] = c < dW ? load_stream<V>(src + c * T::W) : T::zero();
         }
     }
 }
@@ -383,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
                 V s = pre[0][q];
 #pragma unroll
                 for (int p = 1; p < NP; ++p) s = T::add(s, pre[p][q]);
-                T::store(yr + c * T::W, div_exact<V>(T::add(s, acc[q]), ep.div, ep.pad));
+                store_out<V>(yr + c * T::W, div_exact<V>(T::add(s, acc[q]), ep.div, ep.pad));
             }
         } else {
             accumulate<V, G, NV, U, XD>(edges, beg, end, x, lane, dW, acc, xdiv, x_nz);

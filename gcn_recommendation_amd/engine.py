@@ -94,7 +94,8 @@ def load_library(path=None):
     with _lib_lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        # LGCN_LIB: an alternative build of the same ABI (A/B timing of kernel variants)
+        p = path or os.environ.get("LGCN_LIB") or LIB_PATH
         if not os.path.exists(p):
             raise LgcnError(f"liblgcn_engine.so not found at {p}: run `python -c \"import "
                             f"__graft_entry__ as g; g.build()\"` (hipcc --offload-arch=gfx950)")
