@@ -24,6 +24,8 @@
 namespace lgcn_detail {
 int g_rows_per_group = 0;
 int g_unroll = 0;
+int g_mean_prefetch = 0;
+int g_min_groups = 0;
 }  // namespace lgcn_detail
 
 namespace {
@@ -346,6 +348,16 @@ int lgcn_tune(int knob, int value) {
         case LGCN_TUNE_UNROLL: {
             const int old = lgcn_detail::g_unroll;
             if (value >= 0) lgcn_detail::g_unroll = value;
+            return old;
+        }
+        case LGCN_TUNE_MEAN_PREFETCH: {
+            const int old = lgcn_detail::g_mean_prefetch;
+            if (value >= 0) lgcn_detail::g_mean_prefetch = value;
+            return old;
+        }
+        case LGCN_TUNE_MIN_GROUPS: {
+            const int old = lgcn_detail::g_min_groups;
+            if (value >= 0) lgcn_detail::g_min_groups = value;
             return old;
         }
         default:

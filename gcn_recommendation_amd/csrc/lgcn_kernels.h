@@ -18,6 +18,8 @@ namespace lgcn_detail {
 // pairs select a fixed d = 64 variant for A/B timing
 extern int g_rows_per_group;
 extern int g_unroll;
+extern int g_mean_prefetch;  // LGCN_TUNE_MEAN_PREFETCH: 2 = off
+extern int g_min_groups;     // LGCN_TUNE_MIN_GROUPS: 0 = 65536
 
 // one lgcn_spmm_layer launch, geometry already chosen (dW = d / lanes' element width)
 struct LayerArgs {
@@ -242,7 +244,20 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
 //    record wb+l) with the next window prefetched, and reach every lane by shuffles — the only
 //    memory latency left on the critical path is the gather itself;
 //  * U gathers are in flight per group across row boundaries.
-template <typename V, int G, int NV, int MODE, int RPG, int U, int XD>
+// NP > 0 (MEAN epilogue; NV == 1 and dW a power of two, so dW divides G): the bundle's
+// E0..E_{K-1} rows are loaded before its edge stream starts — they do not depend on the gathers,
+// so their latency leaves the flush. Element e of the bundle's row-major [nrows x dW] block sits
+// in lane e % G, register slot e / G; all dW elements of a row share one slot, and a flush
+// fetches them with one shuffle per layer.
+template <typename V>
+__device__ __forceinline__ V shfl_v(V v, int src, int width) {
+    if constexpr (VT<V>::W == 4)
+        return make_float4(__shfl(v.x, src, width), __shfl(v.y, src, width),
+                           __shfl(v.z, src, width), __shfl(v.w, src, width));
+    else return __shfl(v, src, width);
+}
+
+template <typename V, int G, int NV, int MODE, int RPG, int U, int XD, int NP = 0>
 __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                                             const lgcn_edge_t* __restrict__ edges,
                                             const int32_t* __restrict__ row_ids, int32_t n_rows,
@@ -259,6 +274,24 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     // lane l (l < nrows) holds the output row of slot r0 + l (the CSR may be stored in a
     // processing order: slot s holds the edges of row row_ids[s])
     const int32_t orl = (lane < nrows) ? (row_ids ? row_ids[r0 + lane] : r0 + lane) : 0;
+    constexpr bool PRE = MODE == LGCN_EPI_MEAN && NP > 0;
+    static_assert(!PRE || NV == 1, "bundle prefetch: one element per lane and slot");
+    V pre[PRE ? NP : 1][PRE ? RPG : 1];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int s = 0; s < RPG; ++s) {
+            const int e = s * G + lane;
+            const int i = e / dW;
+            const int c = e - i * dW;
+            const int32_t orow = __shfl(orl, min(i, G - 1), G);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const float* src = p == 0 ? seg_row(ep.prev0, orow)
+                                          : ep.prev_dense[p - 1] + (int64_t)orow * ep.ld_prev;
+                pre[p][s] = i < nrows ? load_stream<V>(src + c * T::W) : T::zero();
+            }
+        }
+    }
     const int32_t eend = bnd(nrows);
     auto load_win = [&](int32_t b) {
         return (b + lane < eend) ? load_edge(edges + b + lane) : make_int2(0, 0);
@@ -277,7 +310,26 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     auto flush = [&](int i) {
         const int32_t deg = bnd(i + 1) - bnd(i);
         const int32_t orow = __shfl(orl, i, G);
-        if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, orow, lane, dW, acc, y, ldy);
+        if constexpr (PRE) {
+            // ((E0 + E1) + ... + E_{K-1}) + E_K, then / (K+1) — epilogue_store's order
+            const int s = (i * dW) / G;                 // the row's slot, uniform in the group
+            const int src = (i * dW + lane) & (G - 1);  // lane holding column `lane` of row i
+            V sum = T::zero();
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                V v = pre[p][0];
+#pragma unroll
+                for (int q = 1; q < RPG; ++q)
+                    if (q == s) v = pre[p][q];
+                v = shfl_v<V>(v, src, G);
+                sum = p == 0 ? v : T::add(sum, v);
+            }
+            if (deg <= hub_thr && lane < dW)
+                store_out<V>(y + (int64_t)orow * ldy + lane * T::W,
+                             div_exact<V>(T::add(sum, acc[0]), ep.div, ep.pad));
+        } else {
+            if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, orow, lane, dW, acc, y, ldy);
+        }
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
     };
@@ -428,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void k_layer(
     } else {
         const int64_t r0 = gidx * RPG;
         if (r0 >= n_rows) return;
-        rows_bundle<V, G, NV, MODE, RPG, U, XD>(rowptr, edges, row_ids, n_rows, hub_thr,
+        rows_bundle<V, G, NV, MODE, RPG, U, XD, NP>(rowptr, edges, row_ids, n_rows, hub_thr,
                                                 (int32_t)r0, x, y, ldy, lane, dW, ep, xdiv,
                                                 x_nz);
     }
@@ -646,7 +698,8 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_
     // keep >= ~64k lane groups in the grid: small graphs (the reference's real datasets) run
     // one row per group, Books-scale graphs 15-row bundles (with degree-ordered slots the rows
     // of a bundle have equal length, which also pays for the MEAN epilogue's row reads)
-    const int64_t per = (int64_t)n_rows / 65536;
+    const int64_t per = (int64_t)n_rows /
+                        (lgcn_detail::g_min_groups > 0 ? lgcn_detail::g_min_groups : 65536);
     if (RB <= 1 || lgcn_detail::g_rows_per_group == 1 || per < 2) {
         if (MODE == LGCN_EPI_MEAN && NV <= 2) {  // early-issued E0..E_{K-1} row loads
             if (ep.n_prev == 2) return launch_layer_rpg<V, G, NV, MODE, XD, 1, U1, 2>(LGCN_ARGS);
@@ -654,6 +707,16 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_
             if (ep.n_prev == 4) return launch_layer_rpg<V, G, NV, MODE, XD, 1, U1, 4>(LGCN_ARGS);
         }
         return launch_layer_rpg<V, G, NV, MODE, XD, 1, U1>(LGCN_ARGS);
+    }
+    if constexpr (MODE == LGCN_EPI_MEAN && NV == 1 && G >= 4 && G <= 8) {
+        // small d (featsplit shards): the flush's E0..E_{K-1} row reads are latency on the
+        // critical path; bundles of RM rows prefetch them (RM register slots per layer)
+        constexpr int RM = G >= 8 ? 4 : RB;
+        if (lgcn_detail::g_mean_prefetch != 2 && per >= RM && (dW & (dW - 1)) == 0) {
+            if (ep.n_prev == 2) return launch_layer_rpg<V, G, NV, MODE, XD, RM, UB, 2>(LGCN_ARGS);
+            if (ep.n_prev == 3) return launch_layer_rpg<V, G, NV, MODE, XD, RM, UB, 3>(LGCN_ARGS);
+            if (ep.n_prev == 4) return launch_layer_rpg<V, G, NV, MODE, XD, RM, UB, 4>(LGCN_ARGS);
+        }
     }
     if (per >= RB) return launch_layer_rpg<V, G, NV, MODE, XD, RB, UB>(LGCN_ARGS);
     if constexpr (RB >= 8) {

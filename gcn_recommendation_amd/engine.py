@@ -23,7 +23,7 @@ LGCN_EPI_STORE, LGCN_EPI_MEAN, LGCN_EPI_ADD = 0, 1, 2
 LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
-TUNE_ROWS_PER_GROUP, TUNE_UNROLL = 1, 2
+TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
 ABI_VERSION = 3
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
@@ -106,6 +106,9 @@ def load_library(path=None):
             fn.argtypes = args
         if lib.lgcn_abi_version() != ABI_VERSION:
             raise LgcnError("liblgcn_engine.so ABI version mismatch")
+        # LGCN_MEAN_PREFETCH=off: A/B switch of the MEAN layer's bundle prefetch (same bits)
+        if os.environ.get("LGCN_MEAN_PREFETCH", "").lower() in ("0", "off"):
+            lib.lgcn_tune(TUNE_MEAN_PREFETCH, 2)
         _lib = lib
         return lib
 

@@ -115,6 +115,11 @@ const char* lgcn_error_string(int code);
  * Returns the previous value (value < 0 only queries), or LGCN_EINVAL for an unknown knob. */
 #define LGCN_TUNE_ROWS_PER_GROUP 1  /* rows streamed by one lane group in k_layer (1 = one row) */
 #define LGCN_TUNE_UNROLL         2  /* gathers in flight per lane group (d = 64 variants) */
+#define LGCN_TUNE_MEAN_PREFETCH  3  /* MEAN layer on row bundles of <= 8 lanes per row: the
+                                       bundle's E0..E_{K-1} rows loaded up front (0 = auto = on,
+                                       2 = off) */
+#define LGCN_TUNE_MIN_GROUPS     4  /* row bundles only when n_rows >= 2 x this many lane groups
+                                       (0 = auto = 65536; 1 forces bundles on small graphs) */
 int lgcn_tune(int knob, int value);
 
 /* device properties the host side needs (CU count); returns 0/hipError */

@@ -119,3 +119,16 @@ def test_engine_refuses_missing_library(tmp_path):
             engine.load_library(str(tmp_path / "nope.so"))
         finally:
             engine._lib = saved
+
+
+def test_tune_knobs(lib):
+    """lgcn_tune: every knob answers its previous value (a negative value only queries), an
+    unknown knob is refused; knobs never change results (tested on the GPU)."""
+    for knob in (engine.TUNE_ROWS_PER_GROUP, engine.TUNE_UNROLL, engine.TUNE_MEAN_PREFETCH,
+                 engine.TUNE_MIN_GROUPS):
+        old = lib.lgcn_tune(knob, -1)
+        assert old >= 0
+        assert lib.lgcn_tune(knob, 7) == old
+        assert lib.lgcn_tune(knob, old) == 7
+        assert lib.lgcn_tune(knob, -1) == old
+    assert lib.lgcn_tune(99, 1) == -1

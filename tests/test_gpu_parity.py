@@ -152,6 +152,41 @@ def test_dims_and_layers_bitwise(gpu_device, d, order):
         assert np.array_equal(got, oracle.forward(r, c, v, e0, K)), (d, K)
 
 
+@ORDERS
+@pytest.mark.parametrize("d", [4, 8, 12, 16, 32, 64, 128])
+def test_row_bundles_bitwise(gpu_device, d, order):
+    """Row bundles (a lane group streams RPG consecutive slots: the Books-scale geometry) forced
+    on a small power-law graph (LGCN_TUNE_MIN_GROUPS = 1), with and without the MEAN layer's
+    bundle prefetch (small d), K = 1..4: every row is still the CPU's fp32 chain (exact mode);
+    chunked hub rows are identical with and without the prefetch."""
+    lib = engine.load_library()
+    U, I = 1500, 700
+    u, i = graph.powerlaw_interactions(U, I, 12000, d)
+    rows, cols = graph.edge_lists(u, i, U, I, use_brand=False)
+    r, c, v = graph.normalise(rows, cols, U + I + 40)   # + 40 isolated rows
+    n = U + I + 40
+    e0 = np.random.default_rng(d).standard_normal((n, d)).astype(np.float32)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, c])), torch.from_numpy(v),
+                                  (n, n)).to(gpu_device)
+    g = engine.graph_from_coo(adj)
+    x = [torch.from_numpy(e0).to(gpu_device)]
+    old = lib.lgcn_tune(engine.TUNE_MIN_GROUPS, 1)
+    try:
+        for K in (1, 2, 3, 4):
+            want = oracle.forward(r, c, v, e0, K)
+            chunked = []
+            for pf in (0, 2):
+                lib.lgcn_tune(engine.TUNE_MEAN_PREFETCH, pf)
+                got = engine.propagate_forward(g, x, K, hub_threshold=engine.INT32_MAX)
+                assert np.array_equal(got.cpu().numpy(), want), (d, K, pf)
+                chunked.append(engine.propagate_forward(g, x, K, hub_threshold=24).cpu().numpy())
+            assert np.array_equal(chunked[0], chunked[1]), (d, K)
+            assert_close_normwise(chunked[0], want, what=f"chunked d={d} K={K}")
+    finally:
+        lib.lgcn_tune(engine.TUNE_MIN_GROUPS, old)
+        lib.lgcn_tune(engine.TUNE_MEAN_PREFETCH, 0)
+
+
 def test_segments_and_misaligned_rows(gpu_device):
     """E0 as three segments with unaligned bases (scalar path) == contiguous E0."""
     n1, n2, n3, d = 300, 200, 50, 64

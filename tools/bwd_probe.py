@@ -80,15 +80,13 @@ def main():
     Z = torch.zeros_like(G)
     D = torch.randn_like(G)
     y = torch.empty_like(G)
-    lib = engine.load_library()
-    for order, sc1 in (("degree", 0), ("stored", 0)):
-        lib.lgcn_tune(engine.TUNE_STORE_SC1, sc1)
+    for order in ("degree", "stored"):
         g = engine.graph_from_host_csr(rowptr, c, v, n, dev, order=order)
         for name, X in (("dense", D), ("bpr", G), ("zero", Z)):
             nz, cnt = engine.rows_nonzero([X], d, dev)
             ep = engine._epilogue(engine.LGCN_EPI_ADD, addend=engine.rows_desc([X], d),
                                   div=float(K + 1))
-            row = {"order": order, "sc1": sc1, "G": name, "live_rows": int(cnt.item())}
+            row = {"order": order, "G": name, "live_rows": int(cnt.item())}
             row["dense_ms"] = round(time_layer(g, [X], y, d, ep, thr, args.reps, K + 1.0, None), 3)
             ep.addend_nz = nz.data_ptr()
             row["masked_ms"] = round(time_layer(g, [X], y, d, ep, thr, args.reps, K + 1.0, nz), 3)
@@ -97,9 +95,9 @@ def main():
         st = engine._epilogue(engine.LGCN_EPI_STORE)
         mean = engine._epilogue(engine.LGCN_EPI_MEAN, prev0=engine.rows_desc([D], d),
                                 prev_dense=[Z, G], ld_prev=d, div=float(K + 1))
-        print(json.dumps({"order": order, "sc1": sc1, "mean_ms": round(
+        print(json.dumps({"order": order, "mean_ms": round(
             time_layer(g, [D], y, d, mean, thr, args.reps, 1.0, None), 3)}), flush=True)
-        print(json.dumps({"order": order, "sc1": sc1, "store_ms": round(
+        print(json.dumps({"order": order, "store_ms": round(
             time_layer(g, [D], y, d, st, thr, args.reps, 1.0, None), 3)}), flush=True)
         del g
         torch.cuda.empty_cache()

@@ -1,6 +1,6 @@
 """Per-rank cost of the featsplit decomposition, measured on ONE GPU: at P ranks every rank runs
 the full K-layer propagation over the whole C3 graph on d/P columns, with no exchange. Timing
-the single-GPU forward at d = 64/P for P in 1, 2, 4, 8 predicts the strong-scaling curve of
+the single-GPU forward at d = d_config/P for P in 1, 2, 4, 8 predicts the strong-scaling curve of
 `bench.py --gpus P --mode featsplit` (the ranks do not share anything but the node's power).
 
     python tools/featsplit_sweep.py [--config c3] [--steps 10]
@@ -116,8 +116,8 @@ def main():
             ms = a.elapsed_time(b) / args.steps
             lay = np.array([[x.elapsed_time(y) for x, y in st] for st in evs]).mean(0)
             b_layer = nnz * (4 * d + 8) + 4 * (n + 1) + 4 * n * d
-            p = 64 // d
-            row = {"variant": var, "d": d, "ranks_at_d64": p, "ms_per_step": round(ms, 3),
+            p = cfg["d"] // d
+            row = {"variant": var, "d": d, "ranks": p, "ms_per_step": round(ms, 3),
                    "per_layer_ms": [round(float(x), 3) for x in lay],
                    "store_layer_GBps": round(b_layer / (lay[:-1].mean() / 1e3) / 1e9, 1),
                    "edges_per_s": round(K * nnz / (ms / 1e3), 1)}
@@ -129,7 +129,7 @@ def main():
         torch.cuda.empty_cache()
         base = out[0]["ms_per_step"]
         print(json.dumps({"variant": var, "predicted_featsplit_speedup": {
-            str(r_["ranks_at_d64"]): round(base / r_["ms_per_step"], 2) for r_ in out}}),
+            str(r_["ranks"]): round(base / r_["ms_per_step"], 2) for r_ in out}}),
             flush=True)
 
 
