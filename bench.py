@@ -182,6 +182,98 @@ def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
     return out
 
 
+def leave_last_out(u, i, U):
+    """main.py:201-203: the LAST interaction of every user (in list order) is its val item; the
+    rest is train. Returns (train_u, train_i, val_u, val_i)."""
+    order = np.argsort(u, kind="stable")
+    ends = np.searchsorted(u[order], np.arange(U), side="right") - 1
+    has = np.bincount(u, minlength=U) > 0
+    val = order[ends[has]]
+    keep = np.ones(u.size, bool)
+    keep[val] = False
+    return u[keep], i[keep], u[val], i[val]
+
+
+def bench_recall_trained(dev, epochs, k=20, batch=2048):
+    """Recall@20 / NDCG@20 that mean something (random-init embeddings give ~0 by construction):
+    the C2 power-law graph (BASELINE configs[1] shape) with every user's last interaction held
+    out (main.py:201-203), trained for `epochs` epochs by main.py's loop (main.py:479-531:
+    shuffled (user, pos) batches of 2048, uniform negatives rejected against the user's train
+    items as BPRDataset does (main.py:357-363), model(adj) + bpr_loss_reg + backward + Adam
+    lr=1e-3, reg 1e-4) with the drop-in LightGCN on the engine. Parity: the trained weights are
+    propagated by the engine AND by the reference CPU path (torch.sparse.mm COO, oracle/), and
+    both are scored with main.py's evaluate semantics; the engine's fused top-K is scored too."""
+    from gcn_recommendation_amd import evaluate as E
+    from gcn_recommendation_amd.loss import bpr_loss_reg
+    from models.lightgcn import LightGCN
+    from oracle import oracle
+    cfg = CONFIGS["c2"]
+    U, I, d, K = cfg["users"], cfg["items"], cfg["d"], cfg["K"]
+    u, i = graph.powerlaw_interactions(U, I, cfg["interactions"], cfg["seed"])
+    tu, ti, vu, vi = leave_last_out(u, i, U)
+    adj = graph.build_norm_adj(tu, ti, U, I, 0, use_brand=False, device=dev)
+
+    class Cfg:
+        embedding_dim, n_layers, debug = d, K, False
+    import contextlib
+    import io
+    torch.manual_seed(42)
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = LightGCN(U, I, 0, Cfg()).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    train_keys = np.unique(tu * I + ti)
+    rng = np.random.default_rng(0)
+    steps, t0, loss = 0, time.time(), None
+    for _ in range(epochs):
+        perm = rng.permutation(tu.size)
+        for s0 in range(0, tu.size, batch):
+            b = perm[s0:s0 + batch]
+            bu, bp = tu[b], ti[b]
+            bn = rng.integers(0, I, b.size)
+            while True:  # rejection against the user's train items
+                key = bu * I + bn
+                pos = np.minimum(np.searchsorted(train_keys, key), train_keys.size - 1)
+                hit = train_keys[pos] == key
+                if not hit.any():
+                    break
+                bn[hit] = rng.integers(0, I, int(hit.sum()))
+            users, pi, ni = (torch.from_numpy(x).to(dev) for x in (bu, bp, bn))
+            opt.zero_grad()
+            fu, fi, _, u0, i0 = model(adj, use_brand=False)
+            loss = bpr_loss_reg(fu[users], fi[pi], fi[ni], u0[users], i0[pi], i0[ni], 1e-4)
+            loss.backward()
+            opt.step()
+            steps += 1
+    torch.cuda.synchronize()
+    train_s = time.time() - t0
+    with torch.no_grad():
+        fu, fi, _, _, _ = model(adj)
+        ego = torch.cat([model.user_embedding.weight, model.item_embedding.weight]).cpu()
+    gpu = torch.cat([fu, fi]).cpu().numpy()
+    ref = oracle.reference_forward_torch(adj.cpu(), ego, K).numpy()
+    rec_cpu = oracle.evaluate(ref[:U], ref[U:], vu, vi, tu, ti, k)
+    rec_gpu = oracle.evaluate(gpu[:U], gpu[U:], vu, vi, tu, ti, k)
+    mrow, mit = E.mask_csr(tu, ti, U)
+    _, top = E.topk_fused(fu, fi, vu, mrow, mit, k)
+    hit = top.cpu().numpy() == vi[:, None]
+    found = hit.any(1)
+    ndcg = np.where(found, 1.0 / np.log2(hit.argmax(1) + 2), 0.0)
+    scale = float(np.abs(ref).max())
+    return {"config": "C2 power-law 50k x 50k x 1M, d=64, K=3; val = each user's last "
+                      "interaction (main.py:201-203)",
+            "epochs": epochs, "train_steps": steps, "train_s": round(train_s, 1),
+            "loss_last": float(loss.item()) if loss is not None else None,
+            "val_users": int(vu.size),
+            "recall20_gpu": rec_gpu[0], "ndcg20_gpu": rec_gpu[1],
+            "recall20_cpu_ref": rec_cpu[0], "ndcg20_cpu_ref": rec_cpu[1],
+            "identical": rec_gpu == rec_cpu,
+            "fused_topk": {"recall20": float(found.mean()), "ndcg20": float(ndcg.mean())},
+            "embeddings_normwise_vs_cpu_ref": float(np.abs(gpu - ref).max()) / scale,
+            "what": "weights trained on the GPU through the engine; the same weights propagated "
+                    "by the engine and by the reference CPU path, both scored by main.py's "
+                    "evaluate (oracle restatement); fused_topk = the engine's lgcn_score_topk"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,6 +284,8 @@ def main():
     ap.add_argument("--hub-threshold", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--recall-users", type=int, default=2048)
+    ap.add_argument("--recall-epochs", type=int, default=10,
+                    help="epochs of C2 training for the trained Recall@20 parity (0: skip)")
     ap.add_argument("--train-steps", type=int, default=5,
                     help="also time main.py's training step (forward+BPR+backward+Adam)")
     ap.add_argument("--mode", default="featsplit", choices=["rowpart", "featsplit"],
@@ -430,6 +524,8 @@ def main():
                               "note": "random-init embeddings and random held-out items: recall "
                                       "is ~0 by construction; the top-20 list agreement is the "
                                       "informative parity number"}
+    if args.recall_epochs > 0 and args.config == "c3" and not args.no_cpu_baseline:
+        result["recall20_trained"] = bench_recall_trained(dev, args.recall_epochs)
     print(json.dumps(result), flush=True)
 
 
