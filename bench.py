@@ -290,6 +290,8 @@ def main():
                     help="also time main.py's training step (forward+BPR+backward+Adam)")
     ap.add_argument("--mode", default="featsplit", choices=["rowpart", "featsplit"],
                     help="multi-GPU decomposition (N>1)")
+    ap.add_argument("--no-c4", dest="c4", action="store_false",
+                    help="skip the d=256 K=4 (BASELINE configs[3]) timing on the same graph")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed path even at WORLD_SIZE=1 (testing)")
     args = ap.parse_args()
@@ -418,6 +420,34 @@ def main():
         "wall_s_timed": round(wall, 3), "prep_s": round(prep_s, 2),
         "adjacency_build": builder,
     }
+
+    # BASELINE configs[3] on the same graph (d=256, K=4): the 1-GPU side of the 8-GPU target
+    # (dist.featsplit_c4 times the same forward on d/P columns per rank at N > 1)
+    if args.c4 and not fusion and not B:
+        from gcn_recommendation_amd import dist as D
+        gen4 = torch.Generator(device=dev).manual_seed(1000)
+        x4 = (torch.rand((n, D.C4_D), generator=gen4, device=dev) * 2 - 1) * float(
+            np.sqrt(6.0 / (n + D.C4_D)))
+        for _ in range(2):
+            engine.propagate_forward(g, [x4], D.C4_K, hub_thr)
+        ev4 = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(D.C4_K)] for _ in range(5)]
+        torch.cuda.synchronize()
+        start.record()
+        for s in range(5):
+            engine.propagate_forward(g, [x4], D.C4_K, hub_thr, layer_events=ev4[s])
+        stop.record()
+        torch.cuda.synchronize()
+        ms4 = start.elapsed_time(stop) / 5
+        lay4 = np.array([[a.elapsed_time(b) for a, b in st] for st in ev4]).mean(0)
+        b4 = nnz * (4 * D.C4_D + 8) + 4 * (n + 1) + 4 * n * D.C4_D
+        result["c4_same_graph"] = {
+            "d": D.C4_D, "layers": D.C4_K, "ms_per_step": round(ms4, 3),
+            "edges_per_s": round(D.C4_K * nnz / (ms4 / 1e3), 1),
+            "per_layer_ms": [round(float(x), 3) for x in lay4],
+            "store_layer_frac_of_8TBps": round(b4 / (lay4[:-1].mean() / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
+        del x4
+        torch.cuda.empty_cache()
 
     # backward propagation alone (the K engine layers autograd runs per training batch)
     gsegs = [out[:U].clone(), out[U:].clone()]
