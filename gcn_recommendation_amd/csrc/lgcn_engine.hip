@@ -298,9 +298,20 @@ int spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     }
 }
 
-int hub_combine(const lgcn_hub_row_t* rows, int32_t n, const float* partials, float* y,
+int hub_combine(const lgcn_hub_row_t* rows, int32_t n, int32_t n_pre, float* partials, float* y,
                 int64_t ldy, int32_t d, const lgcn_epilogue_t& ep_in, hipStream_t s) {
     if (n <= 0) return 0;
+    if (n_pre > 0) {  // level 1: runs of partial slots summed into partial slots (plain store)
+        lgcn_epilogue_t st;
+        memset(&st, 0, sizeof(st));
+        st.mode = LGCN_EPI_STORE;
+        st.div = 1.f;
+        const Geo g1 = pick_geo(d, al16(partials) && (d % 4 == 0));
+        CombineF f1{rows, n_pre, partials, partials, d, d, g1.dW, &st, s};
+        if (int e = dispatch_geo(g1, f1)) return e;
+        rows += n_pre;
+        n -= n_pre;
+    }
     const lgcn_epilogue_t ep = with_pow2(ep_in);
     const bool vec_ok = al16(partials) && al16(y) && (ldy % 4 == 0) && epi_aligned(ep);
     const Geo g = pick_geo(d, vec_ok);
@@ -608,13 +619,15 @@ int lgcn_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t d, uint32_t* mask, 
     return dispatch_geo(g, f);
 }
 
-int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
-                     float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
-                     void* stream) {
+int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, int32_t n_pre_rows,
+                     float* partials, float* y, int64_t ldy, int32_t d,
+                     const lgcn_epilogue_t* epi_host, void* stream) {
     if (d < 1 || d > 2048 || n_hub_rows < 0) return LGCN_EINVAL;
+    if (n_pre_rows < 0 || n_pre_rows > n_hub_rows) return LGCN_EINVAL;
     if (int e = check_epi(epi_host)) return e;
     if (n_hub_rows > 0 && (!hub_rows || !partials || !y || ldy < d)) return LGCN_EINVAL;
-    return hub_combine(hub_rows, n_hub_rows, partials, y, ldy, d, *epi_host, S(stream));
+    return hub_combine(hub_rows, n_hub_rows, n_pre_rows, partials, y, ldy, d, *epi_host,
+                       S(stream));
 }
 
 int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
@@ -628,7 +641,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
                            const int32_t* row_ids, int32_t n,
                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                           int32_t n_hub_rows, float* partials, lgcn_rows_t emb, int32_t d,
+                           int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                           lgcn_rows_t emb, int32_t d,
                            int32_t K, float* const* layer_bufs_host, float* out,
                            void* const* ev_host, void* stream) {
     if (int e = valid_geom(n, d)) return e;
@@ -662,7 +676,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1) + 1], s))) return e;
         }
-        if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;
+        if (int e = hub_combine(hub_rows, n_hub_rows, n_pre_rows, partials, y, d, d, ep, s))
+            return e;
     }
     return 0;
 }
@@ -671,7 +686,8 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const int32_t* row_ids, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out,
+                            int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                            lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                             float* grad_e0, void* stream) {
     if (int e = valid_geom(n, d)) return e;
@@ -696,7 +712,8 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
         if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items,
                                partials, h, y, d, d, ep, xdiv, x_nz, s))
             return e;
-        if (int e = hub_combine(hub_rows, n_hub_rows, partials, y, d, d, ep, s)) return e;
+        if (int e = hub_combine(hub_rows, n_hub_rows, n_pre_rows, partials, y, d, d, ep, s))
+            return e;
         h = dense_rows(y, n, d);
         xdiv = 1.f;
         x_nz = nullptr;

@@ -24,12 +24,14 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
 DEFAULT_HUB_THRESHOLD = 128
 DEFAULT_HUB_CHUNK = int(os.environ.get("LGCN_HUB_CHUNK", "256"))
+# Hub rows with more chunks than this are combined in two levels (plan_hubs); 0 = one level
+DEFAULT_HUB_PRE_GROUP = int(os.environ.get("LGCN_HUB_PRE_GROUP", "256"))
 
 
 class RowsT(ctypes.Structure):
@@ -78,12 +80,12 @@ ABI = [
     ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, RowsT, ctypes.c_float,
                                        _P, _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_rows_nonzero", ctypes.c_int, [RowsT, _I32, _I32, _P, _P, _P]),
-    ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _P, _P, _I64, _I32,
+    ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _I32,
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
-    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _P,
+    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _I32, _P,
                                               RowsT, _I32, _I32, _P, _P, _P, _P]),
-    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _P,
+    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _I32, _P,
                                                RowsT, _P, _I32, _I32, _P, _P, _P]),
 ]
 
@@ -203,36 +205,59 @@ def hub_threshold_from_env(default=DEFAULT_HUB_THRESHOLD):
 # graph plan: CSR + hub chunks, built once per adjacency tensor and cached on it
 # ----------------------------------------------------------------------------------------------
 class HubPlan:
-    def __init__(self, threshold, chunk, items, rows, n_slots):
+    def __init__(self, threshold, chunk, items, rows, n_slots, n_hub_rows=0, n_pre=0):
         self.threshold = threshold
         self.chunk = chunk
         self.items = items      # int32 [n_items, 4] device (lgcn_hub_item_t)
-        self.rows = rows        # int32 [n_rows, 4] device (lgcn_hub_row_t)
+        self.rows = rows        # int32 [n_pre + n_rows, 4] device (lgcn_hub_row_t)
         self.n_items = 0 if items is None else items.shape[0]
-        self.n_rows = 0 if rows is None else rows.shape[0]
-        self.n_slots = n_slots
+        self.n_rows = n_hub_rows  # hub rows (final entries, after the n_pre pre-reductions)
+        self.n_pre = n_pre
+        self.n_entries = n_pre + n_hub_rows
+        self.n_slots = n_slots  # partial rows: chunk slots + pre-reduction slots
 
 
-def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None):
+def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_group=None):
     """Cut rows with degree > threshold into `chunk`-edge pieces (host planner, numpy).
-    rowptr_host is in storage (slot) order; row_ids_host maps a slot to its output row."""
+    rowptr_host is in storage (slot) order; row_ids_host maps a slot to its output row.
+
+    A hub row with more than pre_group chunks is combined in two levels: pre-reduction entries
+    (leading the row list) sum runs of pre_group consecutive chunk partials into extra partial
+    slots, and the row's final entry sums those. Without it the combine of a 2.77M-edge row
+    (10.8k partials) is one block's 85-step latency chain, longer than all other rows together."""
+    if pre_group is None:
+        pre_group = DEFAULT_HUB_PRE_GROUP
     deg = np.diff(rowptr_host.astype(np.int64))
     hub = np.nonzero(deg > threshold)[0]
     if threshold >= INT32_MAX or hub.size == 0:
         return HubPlan(threshold, chunk, None, None, 0)
     nch = (deg[hub] + chunk - 1) // chunk
     first = np.concatenate([[0], np.cumsum(nch)[:-1]])
-    n_slots = int(nch.sum())
+    n_chunks = int(nch.sum())
     row_of = np.repeat(hub, nch)
-    k = np.arange(n_slots) - np.repeat(first, nch)
+    k = np.arange(n_chunks) - np.repeat(first, nch)
     beg = rowptr_host[row_of].astype(np.int64) + k * chunk
     end = np.minimum(beg + chunk, rowptr_host[row_of + 1])
     # longest rows first so their combine inputs are ready early; items in slot order
     out_row = hub if row_ids_host is None else row_ids_host[hub]
-    items = np.stack([np.repeat(out_row, nch), beg, end, np.arange(n_slots)], 1).astype(np.int32)
-    rows = np.stack([out_row, first, nch, np.zeros_like(hub)], 1).astype(np.int32)
+    items = np.stack([np.repeat(out_row, nch), beg, end, np.arange(n_chunks)], 1).astype(np.int32)
+    rows = np.stack([out_row, first, nch, np.zeros_like(hub)], 1).astype(np.int64)
+    pre = np.zeros((0, 4), np.int64)
+    if pre_group > 0:
+        big = np.nonzero(nch > pre_group)[0]
+        ng = (nch[big] + pre_group - 1) // pre_group           # pre-reductions per big row
+        gfirst = np.cumsum(ng) - ng
+        n_pre = int(ng.sum())
+        j = np.arange(n_pre) - np.repeat(gfirst, ng)
+        src0 = np.repeat(first[big], ng) + j * pre_group
+        cnt = np.minimum(pre_group, np.repeat(first[big] + nch[big], ng) - src0)
+        pre = np.stack([n_chunks + np.arange(n_pre), src0, cnt, np.ones(n_pre, np.int64)], 1)
+        rows[big, 1] = n_chunks + gfirst
+        rows[big, 2] = ng
+    n_slots = n_chunks + pre.shape[0]
+    table = np.concatenate([pre, rows]).astype(np.int32)
     return HubPlan(threshold, chunk, torch.from_numpy(items).to(device),
-                   torch.from_numpy(rows).to(device), n_slots)
+                   torch.from_numpy(table).to(device), n_slots, hub.size, pre.shape[0])
 
 
 class Graph:
@@ -266,7 +291,7 @@ class Graph:
 
     def hubs(self, threshold, chunk=None):
         chunk = chunk or DEFAULT_HUB_CHUNK
-        key = (threshold, chunk)
+        key = (threshold, chunk, DEFAULT_HUB_PRE_GROUP)
         if key not in self._plans:
             self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device,
                                          self.row_ids_host())
@@ -500,8 +525,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
                                _ptr(partials), x, x_div, _ptr(x_nz), _ptr(y), y.stride(0), d,
                                ctypes.byref(epi), stream), "lgcn_spmm_layer")
     if hp.n_rows:
-        _check(lib.lgcn_hub_combine(_ptr(hp.rows), hp.n_rows, _ptr(partials), _ptr(y), y.stride(0),
-                                    d, ctypes.byref(epi), stream), "lgcn_hub_combine")
+        _check(lib.lgcn_hub_combine(_ptr(hp.rows), hp.n_entries, hp.n_pre, _ptr(partials), _ptr(y),
+                                    y.stride(0), d, ctypes.byref(epi), stream), "lgcn_hub_combine")
     return y
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 3
+#define LGCN_ABI_VERSION 4
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -83,7 +83,10 @@ typedef struct {
     int32_t slot;
 } lgcn_hub_item_t;
 
-/* one long row: its partials occupy slots [first_slot, first_slot + n_slots); row = output row */
+/* one long row: its partials occupy slots [first_slot, first_slot + n_slots); row = output row.
+ * A row list may start with n_pre pre-reduction entries: `row` is then a partial slot that
+ * receives the sum of slots [first_slot, first_slot + n_slots) (two-level combine of rows with
+ * thousands of chunks); pad = 1 marks them (informational). */
 typedef struct {
     int32_t row;
     int32_t first_slot;
@@ -216,10 +219,12 @@ int lgcn_spmm_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32
                     const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
                     const lgcn_epilogue_t* epi_host, void* stream);
 
-/* Finish hub rows: sum each row's partial slots in slot order, apply the epilogue, write Y. */
-int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, const float* partials,
-                     float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
-                     void* stream);
+/* Finish hub rows: entries [0, n_pre_rows) first sum runs of partial slots into other partial
+ * slots (one launch), then every remaining entry sums its slots in a fixed order, applies the
+ * epilogue and writes Y (a second launch). Deterministic. */
+int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, int32_t n_pre_rows,
+                     float* partials, float* y, int64_t ldy, int32_t d,
+                     const lgcn_epilogue_t* epi_host, void* stream);
 
 /* Row-sparsity of a block: mask[(n_rows+31)/32] gets bit r set iff row r holds a value != 0
  * (NaN included); *count (device int32) = number of such rows. No pre-zeroing needed. */
@@ -238,7 +243,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
                            const int32_t* row_ids, int32_t n,
                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                           int32_t n_hub_rows, float* partials, lgcn_rows_t emb, int32_t d,
+                           int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                           lgcn_rows_t emb, int32_t d,
                            int32_t K, float* const* layer_bufs_host, float* out,
                            void* const* ev_host, void* stream);
 
@@ -252,7 +258,8 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const int32_t* row_ids, int32_t n,
                             int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
                             int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, float* partials, lgcn_rows_t grad_out,
+                            int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                            lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                             float* grad_e0, void* stream);
 

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 3
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 4
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -65,10 +65,12 @@ def test_argument_validation_without_gpu(lib):
     ep.mode = engine.LGCN_EPI_MEAN
     ep.n_prev = 18
     ep.div = 2.0
-    assert lib.lgcn_hub_combine(None, 0, None, None, 64, 64, ctypes.byref(ep), None) == -3
+    assert lib.lgcn_hub_combine(None, 0, 0, None, None, 64, 64, ctypes.byref(ep), None) == -3
+    ep.n_prev = 2
+    assert lib.lgcn_hub_combine(None, 4, 5, None, None, 64, 64, ctypes.byref(ep), None) == -1
     assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 64, None, None, None) == -1
     assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 0, None, None, None) == -1
-    assert lib.lgcn_propagate_forward(None, None, None, 5, 0, None, 0, None, 0, None, rows, 64, -1,
+    assert lib.lgcn_propagate_forward(None, None, None, 5, 0, None, 0, None, 0, 0, None, rows, 64, -1,
                                       None, None, None, None) == -1
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,

@@ -187,6 +187,56 @@ def test_row_bundles_bitwise(gpu_device, d, order):
         lib.lgcn_tune(engine.TUNE_MEAN_PREFETCH, 0)
 
 
+@ORDERS
+@pytest.mark.parametrize("thr", [16, "exact"])
+def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, thr):
+    """lgcn_propagate_forward / lgcn_propagate_backward — the one-call entry points a C host
+    binds — equal the per-layer path the Python binding drives, bitwise,
+    with chunked hub rows and two-level combines (pre_group 2); exact mode equals the oracle."""
+    import ctypes
+    monkeypatch.setattr(engine, "DEFAULT_HUB_PRE_GROUP", 2)
+    monkeypatch.setattr(engine, "DEFAULT_HUB_CHUNK", 8)   # hub_d32's rows reach degree 60
+    z = load_case("hub_d32")
+    U, I, B, d, K = case_dims(z)
+    n = U + I + B
+    thr = engine.INT32_MAX if thr == "exact" else thr
+    lib = engine.load_library()
+    P = engine._ptr
+    g = engine.graph_from_coo(_adj(z, gpu_device))
+    segs = [torch.from_numpy(z[f"param/{k}_embedding.weight"]).to(gpu_device)
+            for k in ("user", "item", "brand")]
+    st = engine._stream(gpu_device)
+    hp = g.hubs(thr)
+    if thr == 16:
+        assert hp.n_pre > 0
+    layers = [torch.empty((n, d), device=gpu_device) for _ in range(K - 1)]
+    out = torch.empty((n, d), device=gpu_device)
+    part = torch.empty(max(hp.n_slots, 1) * d, device=gpu_device)
+    bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
+    rc = lib.lgcn_propagate_forward(P(g.rowptr), P(g.edges), P(g.row_ids), n, thr, P(hp.items),
+                                    hp.n_items, P(hp.rows), hp.n_entries, hp.n_pre, P(part),
+                                    engine.rows_desc(segs, d), d, K, ctypes.cast(bufs, ctypes.c_void_p),
+                                    P(out), None, st)
+    assert rc == 0
+    want = engine.propagate_forward(g, segs, K, thr)
+    assert torch.equal(out, want)
+    if thr == engine.INT32_MAX:
+        assert np.array_equal(out.cpu().numpy(),
+                              oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], case_e0(z), K))
+    G = torch.from_numpy(upstream_grad(n, d)).to(gpu_device)
+    gt = g.transpose
+    hpt = gt.hubs(thr)
+    work = torch.empty((n, d), device=gpu_device)
+    ge0 = torch.empty((n, d), device=gpu_device)
+    part_t = torch.empty(max(hpt.n_slots, 1) * d, device=gpu_device)
+    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n, thr,
+                                     P(hpt.items), hpt.n_items, P(hpt.rows), hpt.n_entries,
+                                     hpt.n_pre, P(part_t), engine.rows_desc([G], d), None, d, K,
+                                     P(work), P(ge0), st)
+    assert rc == 0
+    assert torch.equal(ge0, engine.propagate_backward(g, [G], K, thr, sparse="off"))
+
+
 def test_segments_and_misaligned_rows(gpu_device):
     """E0 as three segments with unaligned bases (scalar path) == contiguous E0."""
     n1, n2, n3, d = 300, 200, 50, 64

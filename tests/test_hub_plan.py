@@ -7,9 +7,10 @@ from gcn_recommendation_amd import engine
 def test_plan_covers_hub_rows_exactly():
     deg = np.array([0, 3, 700, 1, 2000, 512, 513])
     rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
-    hp = engine.plan_hubs(rowptr, 512, 256, "cpu")
+    hp = engine.plan_hubs(rowptr, 512, 256, "cpu", pre_group=0)
     items = hp.items.numpy()
     rows = hp.rows.numpy()
+    assert hp.n_pre == 0 and hp.n_rows == hp.n_entries == 3
     assert list(rows[:, 0]) == [2, 4, 6]
     assert hp.n_slots == items.shape[0] == 3 + 8 + 3
     for r, first, n, _ in rows:
@@ -19,6 +20,43 @@ def test_plan_covers_hub_rows_exactly():
         assert (it[1:, 1] == it[:-1, 2]).all()
         assert (it[:, 3] == np.arange(first, first + n)).all()
         assert ((it[:, 2] - it[:, 1]) <= 256).all()
+
+
+def test_two_level_combine_plan():
+    """Rows with more than pre_group chunks: leading pre-reduction entries sum consecutive runs
+    of the row's chunk slots into new slots (after all chunk slots); the row's final entry sums
+    exactly those new slots; rows with few chunks are untouched."""
+    deg = np.array([5, 300, 10 ** 5 + 7, 4096, 1000])
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    hp = engine.plan_hubs(rowptr, 128, 256, "cpu", pre_group=8)
+    items, tab = hp.items.numpy(), hp.rows.numpy()
+    n_chunks = items.shape[0]
+    assert n_chunks == 2 + 391 + 16 + 4
+    pre, fin = tab[:hp.n_pre], tab[hp.n_pre:]
+    assert hp.n_rows == 4 and list(fin[:, 0]) == [1, 2, 3, 4]
+    assert (pre[:, 3] == 1).all() and (fin[:, 3] == 0).all()
+    assert hp.n_pre == 49 + 2 and hp.n_slots == n_chunks + hp.n_pre
+    assert (pre[:, 0] == n_chunks + np.arange(hp.n_pre)).all()
+    covered = np.zeros(n_chunks, int)
+    for tgt, first, n, _ in pre:
+        assert 1 <= n <= 8
+        covered[first:first + n] += 1
+    for r, first, n, _ in fin:
+        if first >= n_chunks:  # two-level row: its slots are pre-reduction targets, in order
+            it = items[(items[:, 0] == r)]
+            src = pre[(pre[:, 0] >= first) & (pre[:, 0] < first + n)]
+            assert src[0, 1] == it[0, 3] and src[-1, 1] + src[-1, 2] == it[-1, 3] + 1
+            assert (src[1:, 1] == src[:-1, 1] + src[:-1, 2]).all()
+        else:
+            assert n <= 8
+            covered[first:first + n] += 1
+    assert (covered == 1).all()  # every chunk partial is summed exactly once
+
+
+def test_two_level_plan_without_big_rows():
+    rowptr = np.array([0, 300, 301, 900], dtype=np.int32)
+    hp = engine.plan_hubs(rowptr, 128, 256, "cpu", pre_group=8)
+    assert hp.n_pre == 0 and hp.n_rows == 2 and hp.n_slots == 2 + 3
 
 
 def test_exact_mode_has_no_hubs():
