@@ -74,6 +74,8 @@ ABI = [
     ("lgcn_adj_finish", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
     ("lgcn_bpr_loss", ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64,
                                      _I32, _I32, ctypes.c_float, _P, _P, _P, _P]),
+    ("lgcn_fusion_prelayer", ctypes.c_int, [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P,
+                                            ctypes.c_float, _P, _I64, _P]),
     ("lgcn_eval_splits", ctypes.c_int, [_I32, _I32, _I32]),
     ("lgcn_score_topk", ctypes.c_int, [_P, _I64, _P, _I32, _P, _I64, _I32, _I32, _P, _P, _I32,
                                        _I32, _P, _P, _P, _P, _P]),

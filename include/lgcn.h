@@ -274,6 +274,17 @@ int lgcn_bpr_loss(const float* u, int64_t ldu, const float* p, int64_t ldp, cons
                   const float* n0, int64_t ldn0, int32_t B, int32_t d, float lambda, float* terms,
                   float* loss, float* grads, void* stream);
 
+/* ---- LightGCN_Fusion item pre-layer (models/lightgcn_fusion.py:45-49) ------------------------ */
+/* out[i,:] = leaky_relu(weight · [id_emb[i,:] | content[i,:]] + bias, slope) for i < n_items,
+ * i.e. F.leaky_relu(nn.Linear(d + c_dim, d)(torch.cat([id, content], 1))) without the
+ * concatenation: exact-f32 MFMA GEMM with the bias and activation fused into its epilogue.
+ * weight: [d x (d + c_dim)] row-major (nn.Linear.weight); bias: [d] or NULL. d in {64, 128},
+ * c_dim in {32, 64, 128}; 16-B aligned rows. */
+int lgcn_fusion_prelayer(const float* id_emb, int64_t ld_id, const float* content, int64_t ld_c,
+                         int32_t n_items, int32_t d, int32_t c_dim, const float* weight,
+                         const float* bias, float slope, float* out, int64_t ld_out,
+                         void* stream);
+
 /* ---- evaluation (main.py:404-439) ----------------------------------------------------------- */
 /* Item splits for lgcn_score_topk: ~2 blocks per CU, >= 2048 items per split, <= 256. */
 int lgcn_eval_splits(int32_t n_users, int32_t n_items, int32_t n_cu);

@@ -3,15 +3,15 @@
 Same constructor (raises without pretrained content embeddings), module registration and RNG
 order (user, item_id, brand embeddings, fusion Linear, then four xavier inits), buffer
 `item_content_embedding`, and 5-tuple. The item pre-fusion `leaky_relu(Linear([id ‖ content]))`
-(lightgcn_fusion.py:45-49) is a small dense GEMM left to torch (hipBLASLt on ROCm); the K-layer
+(lightgcn_fusion.py:45-49) runs as one engine kernel on a HIP device (no concatenation, MFMA GEMM
+with bias + leaky_relu fused, gcn_recommendation_amd.fusion); the K-layer
 propagation + mean (lightgcn_fusion.py:55-59) runs in the MI355X engine, reading
 E0 = [user | fused_item | brand] as three segments.
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
-from gcn_recommendation_amd import engine
+from gcn_recommendation_amd import engine, fusion
 
 
 class LightGCN_Fusion(nn.Module):
@@ -37,8 +37,9 @@ class LightGCN_Fusion(nn.Module):
         self._graph_adj = None
 
     def fused_item_embedding(self):
-        combined = torch.cat([self.item_id_embedding.weight, self.item_content_embedding], dim=1)
-        return F.leaky_relu(self.item_fusion_layer(combined))
+        # lightgcn_fusion.py:45-49; on a HIP device one engine kernel (gcn_recommendation_amd.fusion)
+        return fusion.fused_item_embedding(self.item_id_embedding.weight,
+                                           self.item_content_embedding, self.item_fusion_layer)
 
     def forward(self, adj_mat, use_brand=True):
         user_emb_0 = self.user_embedding.weight
