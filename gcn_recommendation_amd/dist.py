@@ -379,9 +379,13 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
                      dtype=torch.float64, device=dev)
     ms_max, kern_ms, all_ms = _max_over_ranks(t)
-    c4 = None
+    c4 = rp = None
     if mode == "featsplit" and getattr(args, "c4", True):
         c4 = featsplit_c4(plan, world, rank, nnz, n, args, dev, hub_thr)
+    if mode == "featsplit" and getattr(args, "rowpart", True):
+        del plan
+        torch.cuda.empty_cache()
+        rp = rowpart_secondary(r, c, v, n, nnz, K, d, emb_host, world, rank, args, dev, hub_thr)
     value = K * nnz * args.steps / (ms_max / 1e3)
     achieved = b_layer / (kern_ms / 1e3) / 1e9
     return {
@@ -399,4 +403,36 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
                      "kernel": "k_layer store layers, per GPU (max over ranks)",
                      "bytes_per_launch": int(b_layer), "avg_launch_ms": round(kern_ms, 4)},
         **({"c4_same_graph": c4} if c4 else {}),
+        **({"rowpart": rp} if rp else {}),
     }
+
+
+def rowpart_secondary(r, c, v, n, nnz, K, d, emb_host, world, rank, args, dev, hub_thr,
+                      steps=5):
+    """The north_star decomposition measured beside the default one in the same run: row blocks
+    balanced by nnz, every layer's slice all-gathered in place over RCCL (xGMI on one node), the
+    final table gathered too. Local-layer time and exchange time are split by HIP events (max
+    over ranks); the exchange rate is the bytes a rank receives per step / exchange time."""
+    plan = RowPartPlan(r, c, v, n, world, rank, dev)
+    segs = [t.to(dev) for t in emb_host]
+
+    def fn(timed):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(K)] if timed else None
+        rowpart_forward(plan, segs, K, hub_thr, gather_final=True, layer_events=ev)
+        return ev
+    st = min(steps, args.steps)
+    ms, lay = _timed(fn, st, 1, dev)
+    ms_max, local_ms = _max_over_ranks(torch.tensor([ms / st, float(lay.sum(1).mean())],
+                                                    dtype=torch.float64, device=dev))
+    recv = K * (world - 1) * plan.n_max * d * 4  # K-1 layer gathers + the final gather
+    ex_ms = max(ms_max - local_ms, 1e-6)
+    out = {"ms_per_step": round(ms_max, 3), "edges_per_s": round(K * nnz / (ms_max / 1e3), 1),
+           "local_layers_ms": round(local_ms, 3), "exchange_ms": round(ex_ms, 3),
+           "received_bytes_per_step_per_rank": int(recv),
+           "exchange_GBps_per_rank": round(recv / (ex_ms / 1e3) / 1e9, 1),
+           "what": "rowpart (north_star): row blocks + in-place all_gather_into_tensor of every "
+                   "layer's slice (RCCL); exchange = step time - local layer kernels"}
+    del plan, segs
+    torch.cuda.empty_cache()
+    return out
