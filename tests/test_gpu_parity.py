@@ -249,9 +249,11 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, thr):
     assert rc == 0
     want = engine.propagate_forward(g, segs, K, thr)
     assert torch.equal(out, want)
+    ref = oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], case_e0(z), K)
     if thr == engine.INT32_MAX:
-        assert np.array_equal(out.cpu().numpy(),
-                              oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], case_e0(z), K))
+        assert np.array_equal(out.cpu().numpy(), ref)
+    else:  # chunked + two-level combined rows: the north_star tolerance
+        assert_close_normwise(out.cpu().numpy(), ref, what="two-level combine")
     G = torch.from_numpy(upstream_grad(n, d)).to(gpu_device)
     gt = g.transpose
     hpt = gt.hubs(thr)
