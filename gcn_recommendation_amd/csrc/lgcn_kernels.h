@@ -174,6 +174,34 @@ __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges
                                            V (&acc)[NV], float xdiv = 1.f,
                                            const uint32_t* __restrict__ x_nz = nullptr) {
     using T = VT<V>;
+    if constexpr (XD & 4) {
+        // row-sparse X: windows of G records, one per lane; every lane looks up its record's
+        // mask bit (in parallel, the next window already in flight), the group's live edges come
+        // out of the ballot in stored order and are folded in that order
+        const int base = (int)(threadIdx.x & 63) - lane;  // the group's first lane in the wave
+        int2 rec = (beg + lane < end) ? load_edge(edges + beg + lane) : make_int2(0, 0);
+        for (int32_t wb = beg; wb < end; wb += G) {
+            const int2 nrec = (wb + G + lane < end) ? load_edge(edges + wb + G + lane)
+                                                    : make_int2(0, 0);
+            const bool lvb = wb + lane < end && row_live(x_nz, rec.x);
+            unsigned long long m = __ballot(lvb) >> base;
+            if constexpr (G < 64) m &= (1ull << G) - 1;
+            while (m) {
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                const int c = __shfl(rec.x, i, G);
+                const float v = __int_as_float(__shfl(rec.y, i, G));
+                const float* rp = seg_row(x, c);
+#pragma unroll
+                for (int q = 0; q < NV; ++q) {
+                    const int cc = lane + q * G;
+                    if (cc < dW) acc[q] = T::fma(v, load_x<V, XD>(rp + cc * T::W, xdiv), acc[q]);
+                }
+            }
+            rec = nrec;
+        }
+        return;
+    }
     for (int32_t j = beg; j < end; j += U) {
         const int n = min(U, end - j);
         int2 e[U];
@@ -305,8 +333,15 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     int32_t j = bnd(0);
     if (lend - j > hub_thr) j = lend;        // hub rows: edges owned by the chunk path
     int32_t wb = j;                          // window base
+    // XD & 4 (row-sparse X): each lane looks up the mask bit of ITS record once per window (one
+    // round trip per G edges, in parallel) instead of every lane per edge; edges read it by shuffle
+    auto win_live = [&](const int2& w, int32_t b) -> int {
+        if constexpr (XD & 4) return (b + lane < eend && row_live(x_nz, w.x)) ? 1 : 0;
+        else return 1;
+    };
     int2 win = load_win(wb);
     int2 nxt = load_win(wb + G);
+    int wlv = win_live(win, wb);
     auto flush = [&](int i) {
         const int32_t deg = bnd(i + 1) - bnd(i);
         const int32_t orow = __shfl(orl, i, G);
@@ -337,6 +372,7 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
         int col[U];
         float val[U];
         int rid[U];
+        int lv[U];
         int cnt = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -351,6 +387,7 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
             rid[u] = lr;
             col[u] = 0;
             val[u] = 0.f;
+            lv[u] = 0;
             if (lr < nrows) {
                 if (j >= wb + G) {
                     if (j < wb + 2 * G) {
@@ -361,10 +398,12 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                         win = load_win(wb);
                     }
                     nxt = load_win(wb + G);
+                    wlv = win_live(win, wb);
                 }
                 const int idx = j - wb;
                 col[u] = __shfl(win.x, idx, G);
                 val[u] = __int_as_float(__shfl(win.y, idx, G));
+                if constexpr (XD & 4) lv[u] = __shfl(wlv, idx, G);
                 ++j;
                 ++cnt;
             }
@@ -372,7 +411,7 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
         bool live[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if constexpr (XD & 4) live[u] = u < cnt && row_live(x_nz, col[u]);
+            if constexpr (XD & 4) live[u] = u < cnt && lv[u];
             else live[u] = u < cnt;
         }
         V xv[U][NV];

@@ -312,7 +312,7 @@ def test_unsorted_coo_with_duplicates(gpu_device, order):
 
 
 @ORDERS
-@pytest.mark.parametrize("d", [64, 12])
+@pytest.mark.parametrize("d", [64, 128, 16, 12])
 def test_row_sparse_backward_bitwise(gpu_device, order, d):
     """A BPR-style upstream gradient (a few live rows, one row of -0.0, the rest +0): the
     masked backward (first layer gathers only live rows, epilogues skip zero rows) gives exactly
