@@ -238,7 +238,7 @@ __device__ __forceinline__ void accumulate(const lgcn_edge_t* __restrict__ edges
 template <typename V, int G, int NV, int MODE>
 __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_t row, int lane,
                                                int dW, V (&acc)[NV], float* __restrict__ y,
-                                               int64_t ldy) {
+                                               int64_t ldy, int alive = -1) {
     using T = VT<V>;
     float* yr = y + (int64_t)row * ldy;
 #pragma unroll
@@ -256,7 +256,8 @@ __device__ __forceinline__ void epilogue_store(const lgcn_epilogue_t& ep, int32_
         } else if constexpr (MODE == LGCN_EPI_ADD) {
             // Horner step: (Z / div) + Â·X, Z read in place (segments), Z / div rounded once.
             // A row outside addend_nz is all ±0: ±0/div + out == out (out is never -0).
-            if (!ep.addend_nz || row_live(ep.addend_nz, row))
+            // alive: the row's addend_nz bit when the caller looked it up ahead, else -1
+            if (alive >= 0 ? alive != 0 : (!ep.addend_nz || row_live(ep.addend_nz, row)))
                 out = T::add(div_exact<V>(T::load(seg_row(ep.addend, row) + c * T::W), ep.div,
                                           ep.pad), out);
         }
@@ -302,6 +303,11 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
     // lane l (l < nrows) holds the output row of slot r0 + l (the CSR may be stored in a
     // processing order: slot s holds the edges of row row_ids[s])
     const int32_t orl = (lane < nrows) ? (row_ids ? row_ids[r0 + lane] : r0 + lane) : 0;
+    // ADD: the addend_nz bits of the bundle's rows, looked up once in parallel (lane l: row l)
+    // rather than one dependent lookup per flush
+    int alv = 1;
+    if constexpr (MODE == LGCN_EPI_ADD)
+        alv = (ep.addend_nz && lane < nrows) ? (int)row_live(ep.addend_nz, orl) : 1;
     constexpr bool PRE = MODE == LGCN_EPI_MEAN && NP > 0;
     static_assert(!PRE || NV == 1, "bundle prefetch: one element per lane and slot");
     V pre[PRE ? NP : 1][PRE ? RPG : 1];
@@ -363,7 +369,9 @@ __device__ __forceinline__ void rows_bundle(const int32_t* __restrict__ rowptr,
                 store_out<V>(y + (int64_t)orow * ldy + lane * T::W,
                              div_exact<V>(T::add(sum, acc[0]), ep.div, ep.pad));
         } else {
-            if (deg <= hub_thr) epilogue_store<V, G, NV, MODE>(ep, orow, lane, dW, acc, y, ldy);
+            const int al = MODE == LGCN_EPI_ADD ? __shfl(alv, i, G) : -1;
+            if (deg <= hub_thr)
+                epilogue_store<V, G, NV, MODE>(ep, orow, lane, dW, acc, y, ldy, al);
         }
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
