@@ -23,7 +23,10 @@
 
 namespace {
 
-constexpr int kWaves = 4;
+#ifndef LGCN_EVAL_WAVES
+#define LGCN_EVAL_WAVES 4
+#endif
+constexpr int kWaves = LGCN_EVAL_WAVES;  // waves (x 32 users) per block: they share item tiles
 constexpr int kUsersPerWave = 32;
 constexpr int kCap = 64;     // candidate buffer per user
 constexpr int kCompact = 32; // compact when a buffer holds more than this (one tile adds <= 32)
@@ -287,6 +290,13 @@ int lgcn_score_topk(const float* user_emb, int64_t ld_u, const int32_t* users, i
     if (split_len == 0) split_len = 32;
     const dim3 grid((n_users + kWaves * kUsersPerWave - 1) / (kWaves * kUsersPerWave), n_splits);
     const size_t lds = sizeof(WaveState) * kWaves;
+    {
+        const hipError_t ea = hipFuncSetAttribute(
+            d == 64 ? reinterpret_cast<const void*>(k_score_topk<64>)
+                    : reinterpret_cast<const void*>(k_score_topk<128>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return (int)ea;
+    }
     if (d == 64)
         hipLaunchKernelGGL(k_score_topk<64>, grid, dim3(kWaves * 64), lds, s, user_emb, ld_u, users,
                            n_users, item_emb, ld_i, n_items, split_len, mask_rowptr, mask_items, k,
