@@ -103,9 +103,10 @@ def test_bpr_training_step_matches_reference(gpu_device):
 
 
 def test_fusion_model_vs_reference(gpu_device):
-    """LightGCN_Fusion: the Linear runs on hipBLASLt (not bitwise to MKL); the propagation of
-    its output is checked bitwise against the oracle on the same E0, and the final embeddings
-    within 1e-5 of the reference's."""
+    """LightGCN_Fusion: the pre-layer runs on the engine's MFMA kernel (not bitwise to MKL); the
+    propagation of its output is checked bitwise against the oracle on the same E0, the final
+    embeddings and the reference's gradients (fusion Linear weight/bias in full, the embedding
+    tables' first rows) within 1e-5 of the reference's."""
     z = load_case("c1_fusion")
     U, I, B, d, K = case_dims(z)
     m = _model(z, gpu_device, fusion=True)
@@ -118,8 +119,15 @@ def test_fusion_model_vs_reference(gpu_device):
                         m.brand_embedding.weight]).cpu().numpy()
     want = oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], e0, K)
     assert np.array_equal(final, want)
-    (torch.cat([fu, fi, fb]).sum()).backward()
-    assert m.item_fusion_layer.weight.grad is not None
+    G = torch.from_numpy(upstream_grad(U + I + B, d)).to(gpu_device)
+    (torch.cat([fu, fi, fb]) * G).sum().backward()
+    for n, p in m.named_parameters():
+        g = p.grad.cpu().numpy()
+        if "full/grad/" + n in z.files:
+            assert_close_normwise(g, z["full/grad/" + n], what="grad " + n)
+        else:
+            np.testing.assert_allclose(g[:4], z["head/grad/" + n], rtol=1e-5,
+                                       atol=1e-5 * float(z["absmax/grad/" + n]))
 
 
 @pytest.mark.parametrize("d,c", [(64, 32), (64, 64), (64, 128), (128, 32), (128, 64),
