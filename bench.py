@@ -181,22 +181,22 @@ def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
     return out
 
 
-def leave_last_out(u, i, U):
-    """main.py:201-203: the LAST interaction of every user (in list order) is its val item; the
-    rest is train. Returns (train_u, train_i, val_u, val_i)."""
-    order = np.argsort(u, kind="stable")
-    ends = np.searchsorted(u[order], np.arange(U), side="right") - 1
-    has = np.bincount(u, minlength=U) > 0
-    val = order[ends[has]]
-    keep = np.ones(u.size, bool)
-    keep[val] = False
-    return u[keep], i[keep], u[val], i[val]
+def val_split(u, i):
+    """main.py:201-203 verbatim: rank = groupby(user).rank(method="first", ascending=False) over
+    the constant user column; rank 1 is the validation row, the rest is train. With pandas'
+    "first" tie order that is each user's FIRST row in list order. Returns
+    (train_u, train_i, val_u, val_i)."""
+    import pandas as pd
+    df = pd.DataFrame({"user_idx": u, "item_idx": i})
+    rank = df.groupby("user_idx")["user_idx"].rank(method="first", ascending=False).to_numpy()
+    val = rank == 1
+    return u[~val], i[~val], u[val], i[val]
 
 
 def bench_recall_trained(dev, epochs, k=20, batch=2048):
     """Recall@20 / NDCG@20 that mean something (random-init embeddings give ~0 by construction):
-    the C2 power-law graph (BASELINE configs[1] shape) with every user's last interaction held
-    out (main.py:201-203), trained for `epochs` epochs by main.py's loop (main.py:479-531:
+    the C2 power-law graph (BASELINE configs[1] shape) with main.py's validation split held out
+    (main.py:201-203: one row per user), trained for `epochs` epochs by main.py's loop (main.py:479-531:
     shuffled (user, pos) batches of 2048, uniform negatives rejected against the user's train
     items as BPRDataset does (main.py:357-363), model(adj) + bpr_loss_reg + backward + Adam
     lr=1e-3, reg 1e-4) with the drop-in LightGCN on the engine. Parity: the trained weights are
@@ -209,7 +209,7 @@ def bench_recall_trained(dev, epochs, k=20, batch=2048):
     cfg = CONFIGS["c2"]
     U, I, d, K = cfg["users"], cfg["items"], cfg["d"], cfg["K"]
     u, i = graph.powerlaw_interactions(U, I, cfg["interactions"], cfg["seed"])
-    tu, ti, vu, vi = leave_last_out(u, i, U)
+    tu, ti, vu, vi = val_split(u, i)
     adj = graph.build_norm_adj(tu, ti, U, I, 0, use_brand=False, device=dev)
 
     class Cfg:
@@ -258,8 +258,8 @@ def bench_recall_trained(dev, epochs, k=20, batch=2048):
     found = hit.any(1)
     ndcg = np.where(found, 1.0 / np.log2(hit.argmax(1) + 2), 0.0)
     scale = float(np.abs(ref).max())
-    return {"config": "C2 power-law 50k x 50k x 1M, d=64, K=3; val = each user's last "
-                      "interaction (main.py:201-203)",
+    return {"config": "C2 power-law 50k x 50k x 1M, d=64, K=3; val = main.py:201-203's split "
+                      "(groupby-rank 1: each user's first row)",
             "epochs": epochs, "train_steps": steps, "train_s": round(train_s, 1),
             "loss_last": float(loss.item()) if loss is not None else None,
             "val_users": int(vu.size),

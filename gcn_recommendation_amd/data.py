@@ -32,7 +32,9 @@ def load_preprocessed_data(data_dir, device, use_brand=True, debug=False, verbos
         sample_users = np.random.choice(unique_users, size=sample_size, replace=False)
         all_train_df = all_train_df[all_train_df["user_idx"].isin(sample_users)]
         test_df = test_df[test_df["user_idx"].isin(sample_users)]
-    # main.py:201-203: the last row of each user (file order) is the validation item
+    # main.py:201-203 verbatim: groupby(user).rank(method="first", ascending=False) over the
+    # constant user column ranks a user's rows by appearance, so rank 1 — the validation row —
+    # is the user's FIRST row in file order (tests/test_data_loader.py pins this)
     all_train_df = all_train_df.copy()
     all_train_df["rank"] = all_train_df.groupby("user_idx")["user_idx"].rank(method="first",
                                                                            ascending=False)

@@ -8,7 +8,7 @@ import pandas as pd
 import pytest
 import torch
 
-from conftest import load_case
+from conftest import ROOT, load_case
 from gcn_recommendation_amd import data
 
 
@@ -64,3 +64,16 @@ def test_loader_device_matches_reference(tmp_path, brand, gpu_device):
 def test_loader_missing_stats(tmp_path):
     with pytest.raises(FileNotFoundError):
         data.load_preprocessed_data(str(tmp_path), "cpu")
+
+
+def test_bench_val_split_is_main_py_split():
+    """bench.val_split (the trained-Recall@20 block) is main.py:201-203's split: the row ranked
+    1 by groupby(user).rank(method="first", ascending=False) — each user's FIRST row."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    u = np.array([0, 1, 0, 2, 1, 0, 3])
+    i = np.array([5, 6, 7, 8, 9, 10, 11])
+    tu, ti, vu, vi = bench.val_split(u, i)
+    assert list(zip(vu, vi)) == [(0, 5), (1, 6), (2, 8), (3, 11)]
+    assert list(zip(tu, ti)) == [(0, 7), (1, 9), (0, 10)]
