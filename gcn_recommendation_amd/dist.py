@@ -264,14 +264,31 @@ class FeatSplitPlan:
         return y_slot[self.inv]
 
 
+class _AllReduceSum(torch.autograd.Function):
+    """Sum of every rank's partials (one all_reduce). Every rank then evaluates the same loss
+    of the same sums, so d loss / d (local partial) is the incoming gradient itself: the
+    backward passes it through unchanged, with no collective."""
+
+    @staticmethod
+    def forward(ctx, part):
+        out = part.clone()
+        dist.all_reduce(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 def bpr_loss_featsplit(u_slice, p_slice, n_slice, u0_slice, p0_slice, n0_slice, lambda_reg):
     """bpr_loss_reg (main.py:366-402) on column-sharded rows: partial dot products and partial
-    squared norms are summed over ranks with ONE all_reduce of 2B+1 floats."""
+    squared norms are summed over ranks with ONE all_reduce of 2B+1 floats; differentiable —
+    loss.backward() on every rank gives each rank the gradient of its own columns."""
     B = u_slice.shape[0]
     part = torch.cat([(u_slice * p_slice).sum(1), (u_slice * n_slice).sum(1),
                       (u0_slice.pow(2).sum() + p0_slice.pow(2).sum() +
                        n0_slice.pow(2).sum()).reshape(1)])
-    dist.all_reduce(part)
+    part = _AllReduceSum.apply(part)
     pos, neg, sq = part[:B], part[B:2 * B], part[2 * B]
     bpr = -torch.mean(torch.log(torch.sigmoid(pos - neg) + 1e-8))
     return bpr + lambda_reg * sq / float(B)

@@ -71,11 +71,24 @@ def _worker(rank, world, port, name, q):
         fin = torch.from_numpy(want)
         fu, fi = fin[:U], fin[U:U + I]
         u0, i0 = segs[0], segs[1]
+        fu = fu.clone().requires_grad_()
+        fi = fi.clone().requires_grad_()
+        u0, i0 = u0.clone().requires_grad_(), i0.clone().requires_grad_()
         ref = bpr_loss_reg(fu[bu], fi[bp], fi[bn], u0[bu], i0[bp], i0[bn], 1e-4)
-        mu, mi = mine[:U], mine[U:U + I]
-        su0, si0 = sl[0], sl[1]
+        ref.backward()
+        mu = mine[:U].clone().requires_grad_()
+        mi = mine[U:U + I].clone().requires_grad_()
+        su0, si0 = sl[0].clone().requires_grad_(), sl[1].clone().requires_grad_()
         loss = D.bpr_loss_featsplit(mu[bu], mi[bp], mi[bn], su0[bu], si0[bp], si0[bn], 1e-4)
+        loss.backward()
         out["bpr_rel_err"] = float(abs(loss.item() - ref.item()) / abs(ref.item()))
+        # each rank's gradients == its columns of the full-row gradients
+        gerr = 0.0
+        for got, full in ((mu.grad, fu.grad), (mi.grad, fi.grad), (su0.grad, u0.grad),
+                          (si0.grad, i0.grad)):
+            w = full[:, c0:c1]
+            gerr = max(gerr, float((got - w).abs().max() / max(float(full.abs().max()), 1e-30)))
+        out["bpr_grad_err"] = gerr
         D.shutdown()
         q.put((rank, out))
     except Exception as e:  # surface worker failures to the parent
@@ -100,6 +113,7 @@ def test_rowpart_and_featsplit_world2(name):
         assert out["rowpart_bitwise"], (rk, out)
         assert out["featsplit_bitwise"], (rk, out)
         assert out["bpr_rel_err"] < 1e-6, out
+        assert out["bpr_grad_err"] < 1e-5, out
 
 
 def test_balanced_bounds_and_layout():
