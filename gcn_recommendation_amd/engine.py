@@ -29,7 +29,17 @@ ABI_VERSION = 4
 # Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
 # longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
 DEFAULT_HUB_THRESHOLD = 128
-DEFAULT_HUB_CHUNK = int(os.environ.get("LGCN_HUB_CHUNK", "256"))
+# Edges per hub chunk: LGCN_HUB_CHUNK, else by graph size (hub_chunk_for). A chunk is one lane
+# group's sequential chain, so it must stay short against the whole layer: on the C2 graph
+# (1.6M nonzeros, 0.07-0.1 ms per layer) 128-edge chunks run the forward 0.318 -> 0.224 ms,
+# on C3 (56M) 256 is best (tools/tune.py).
+DEFAULT_HUB_CHUNK = int(os.environ.get("LGCN_HUB_CHUNK", "0")) or None
+
+
+def hub_chunk_for(nnz):
+    if DEFAULT_HUB_CHUNK:
+        return DEFAULT_HUB_CHUNK
+    return 256 if nnz >= 8_000_000 else 128
 # Hub rows with more chunks than this are combined in two levels (plan_hubs); 0 = one level
 DEFAULT_HUB_PRE_GROUP = int(os.environ.get("LGCN_HUB_PRE_GROUP", "256"))
 
@@ -292,7 +302,7 @@ class Graph:
         return self._row_ids_host
 
     def hubs(self, threshold, chunk=None):
-        chunk = chunk or DEFAULT_HUB_CHUNK
+        chunk = chunk or hub_chunk_for(self.nnz)
         key = (threshold, chunk, DEFAULT_HUB_PRE_GROUP)
         if key not in self._plans:
             self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device,
