@@ -291,6 +291,8 @@ def main():
                     help="multi-GPU decomposition (N>1)")
     ap.add_argument("--no-c4", dest="c4", action="store_false",
                     help="skip the d=256 K=4 (BASELINE configs[3]) timing on the same graph")
+    ap.add_argument("--no-dist-backward", dest="backward", action="store_false",
+                    help="N > 1: skip the featsplit backward timing")
     ap.add_argument("--no-rowpart", dest="rowpart", action="store_false",
                     help="N > 1: skip the secondary rowpart (per-layer RCCL all-gather) timing")
     ap.add_argument("--force-dist", action="store_true",

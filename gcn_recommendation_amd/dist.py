@@ -255,6 +255,33 @@ class FeatSplitPlan:
         return engine.propagate_forward(self.graph, [x_slot], K, hub_thr,
                                         layer_events=layer_events)
 
+    def attach_transpose(self, rowptr, cols, vals):
+        """Âᵀ in the same slot space, for the backward of a shard (dE0 = Σ_k (Âᵀ)^k G/(K+1)):
+        the CSR of Âᵀ with each row in the order autograd sums it (stable by column), ordered
+        by degree — the same slot order as Â's, since the pattern is symmetric — and relabelled."""
+        n = self.n
+        rowptr = np.asarray(rowptr, dtype=np.int64)
+        cols = np.asarray(cols, dtype=np.int64)
+        vals = np.asarray(vals, dtype=np.float32)
+        rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr))
+        order = np.argsort(cols, kind="stable")
+        rt = cols[order]
+        rpt = np.searchsorted(rt, np.arange(n + 1)).astype(np.int32)
+        gt = engine.graph_from_host_csr(rpt, rows[order], vals[order], n, self.device,
+                                        order="degree")
+        if not torch.equal(gt.row_ids.long(), self.perm):
+            raise engine.LgcnError("featsplit: the transpose's slot order differs from Â's "
+                                   "(non-symmetric pattern)")
+        self.graph.transpose, _ = engine.relabel_slots(gt)
+        return self
+
+    def backward(self, g_slot, K, hub_thr=None, sparse=None):
+        """dE0 of this rank's columns (slot order) for its columns of the upstream gradient
+        (slot order): the engine backward on Âᵀ in slot space. No exchange."""
+        if self.graph.transpose is None:
+            raise engine.LgcnError("FeatSplitPlan.backward needs attach_transpose() first")
+        return engine.propagate_backward(self.graph, [g_slot], K, hub_thr, sparse=sparse)
+
     def slots(self, ids):
         """Slot positions of node ids (for gathering batch rows out of a slot-space table)."""
         return self.inv[ids]
@@ -328,6 +355,34 @@ def _max_over_ranks(t):
 C4_D, C4_K = 256, 4
 
 
+def featsplit_backward_timing(plan, rowptr, c, v, x_slot, K, args, dev, hub_thr):
+    """The training backward of a featsplit rank (its d/P columns of dE0 through Âᵀ in slot
+    space, no exchange) for a dense upstream gradient, max over ranks. Reported, never fatal:
+    the headline forward line is printed either way."""
+    err = None
+    try:
+        plan.attach_transpose(rowptr, c, v)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
+    # every rank takes the same branch (a one-sided failure must not strand the others in a
+    # collective): proceed only if the transpose was built everywhere
+    (failed,) = _max_over_ranks(torch.tensor([1.0 if err else 0.0], dtype=torch.float64,
+                                             device=dev))
+    if failed:
+        plan.graph.transpose = None
+        return {"error": err or "the transpose failed on another rank"}
+    g = torch.randn_like(x_slot)
+    ms, _ = _timed(lambda timed: (plan.backward(g, K, hub_thr, sparse="off"),
+                                  [] if timed else None)[1], args.steps, args.warmup, dev)
+    (ms_max,) = _max_over_ranks(torch.tensor([ms / args.steps], dtype=torch.float64, device=dev))
+    del g
+    plan.graph.transpose = None
+    torch.cuda.empty_cache()
+    return {"ms_per_step": round(ms_max, 4),
+            "propagated_edges_per_s": round(K * plan.graph.nnz / (ms_max / 1e3), 1),
+            "what": "dE0 = sum_k (Â^T)^k G/(K+1) on each rank's columns (dense G)"}
+
+
 def featsplit_c4(plan, world, rank, nnz, n, args, dev, hub_thr):
     """BASELINE configs[3] on the same graph (full Books shape, d=256, K=4 — the configuration
     BASELINE.md sets the >= 6x 8-GPU target on): this rank's d/P = 256/P columns, timed like
@@ -396,7 +451,9 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
                      dtype=torch.float64, device=dev)
     ms_max, kern_ms, all_ms = _max_over_ranks(t)
-    c4 = rp = None
+    c4 = rp = bwd = None
+    if mode == "featsplit" and getattr(args, "backward", True):
+        bwd = featsplit_backward_timing(plan, rowptr, c, v, x_slot, K, args, dev, hub_thr)
     if mode == "featsplit" and getattr(args, "c4", True):
         c4 = featsplit_c4(plan, world, rank, nnz, n, args, dev, hub_thr)
     if mode == "featsplit" and getattr(args, "rowpart", True):
@@ -419,6 +476,7 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
                      "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
                      "kernel": "k_layer store layers, per GPU (max over ranks)",
                      "bytes_per_launch": int(b_layer), "avg_launch_ms": round(kern_ms, 4)},
+        **({"backward": bwd} if bwd else {}),
         **({"c4_same_graph": c4} if c4 else {}),
         **({"rowpart": rp} if rp else {}),
     }

@@ -531,6 +531,16 @@ def test_dist_rowpart_and_featsplit_kernels_on_gpu(gpu_device, order):
             assert np.array_equal(got, want)
     ids = torch.arange(n, device=gpu_device)
     assert torch.equal(plan.perm[plan.slots(ids)], ids)
+    # featsplit backward: each rank's columns of dE0 through Âᵀ in slot space == the oracle
+    plan.attach_transpose(rowptr, c, v)
+    G = upstream_grad(n, d)
+    want_g = oracle.backward(r, c, v, G, K)
+    cols_b = []
+    for p in range(P):
+        _, (c0, c1) = plan.shard(segs, P, p)
+        gs = torch.from_numpy(np.ascontiguousarray(G[:, c0:c1])).to(gpu_device)[plan.perm]
+        cols_b.append(plan.unshard(plan.backward(gs.contiguous(), K, thr, sparse="off")).cpu().numpy())
+    assert np.array_equal(np.concatenate(cols_b, 1), want_g)
 
 
 @pytest.mark.parametrize("name", CASES + ["c1_fusion"])
