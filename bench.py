@@ -324,6 +324,7 @@ def main():
 
     if world > 1 or args.force_dist:
         from gcn_recommendation_amd import dist
+        args.users, args.items = cfg["users"], cfg["items"]
         result = dist.bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr)
         if rank == 0:
             print(json.dumps(result), flush=True)

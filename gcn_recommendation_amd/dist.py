@@ -376,11 +376,60 @@ def featsplit_backward_timing(plan, rowptr, c, v, x_slot, K, args, dev, hub_thr)
                                   [] if timed else None)[1], args.steps, args.warmup, dev)
     (ms_max,) = _max_over_ranks(torch.tensor([ms / args.steps], dtype=torch.float64, device=dev))
     del g
+    out = {"ms_per_step": round(ms_max, 4),
+           "propagated_edges_per_s": round(K * plan.graph.nnz / (ms_max / 1e3), 1),
+           "what": "dE0 = sum_k (Â^T)^k G/(K+1) on each rank's columns (dense G)"}
+    if getattr(args, "train_steps", 0) > 0:
+        out["train_step"] = featsplit_train_timing(plan, x_slot, K, args, dev, hub_thr)
     plan.graph.transpose = None
     torch.cuda.empty_cache()
-    return {"ms_per_step": round(ms_max, 4),
-            "propagated_edges_per_s": round(K * plan.graph.nnz / (ms_max / 1e3), 1),
-            "what": "dE0 = sum_k (Â^T)^k G/(K+1) on each rank's columns (dense G)"}
+    return out
+
+
+class _ShardPropagate(torch.autograd.Function):
+    """A featsplit rank's forward (its columns, slot space) with the engine backward."""
+
+    @staticmethod
+    def forward(ctx, plan, K, hub_thr, x_slot):
+        ctx.plan, ctx.K, ctx.thr = plan, K, hub_thr
+        return plan.forward(x_slot.detach(), K, hub_thr)
+
+    @staticmethod
+    def backward(ctx, g):
+        return None, None, None, ctx.plan.backward(g.contiguous(), ctx.K, ctx.thr)
+
+
+def featsplit_train_timing(plan, x_slot, K, args, dev, hub_thr, batch=2048):
+    """main.py's training step (main.py:488-531) on P ranks: every rank propagates its columns,
+    gathers the batch rows of its shard, the sharded BPR loss reduces partial dots (one
+    all_reduce), the backward runs on the shard's columns, Adam updates the shard. Identical
+    batches on every rank (same seed). Edges/s = 2K·nnz / t, max over ranks."""
+    w = torch.nn.Parameter(x_slot.clone())
+    opt = torch.optim.Adam([w], lr=1e-3)
+    U, I = args.users, args.items
+    rng = np.random.default_rng(0)
+    batches = [tuple(plan.slots(torch.from_numpy(a).to(dev)) for a in (
+        rng.integers(0, U, batch), U + rng.integers(0, I, batch), U + rng.integers(0, I, batch)))
+        for _ in range(args.train_steps + 2)]
+    it = iter(batches)
+
+    def step(timed):
+        su, sp, sn = next(it)
+        opt.zero_grad()
+        out = _ShardPropagate.apply(plan, K, hub_thr, w)
+        loss = bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
+        loss.backward()
+        opt.step()
+        return [] if timed else None
+    ms, _ = _timed(step, args.train_steps, 2, dev)
+    (ms_max,) = _max_over_ranks(torch.tensor([ms / args.train_steps], dtype=torch.float64,
+                                             device=dev))
+    del w, opt
+    return {"ms_per_step": round(ms_max, 3),
+            "propagated_edges_per_s": round(2 * K * plan.graph.nnz / (ms_max / 1e3), 1),
+            "batch": batch, "optimizer": "Adam(lr=1e-3) on the rank's shard",
+            "what": "main.py:488-531 on P ranks: shard forward + batch gathers + sharded BPR loss "
+                    "(one all_reduce) + shard backward + Adam"}
 
 
 def featsplit_c4(plan, world, rank, nnz, n, args, dev, hub_thr):

@@ -678,3 +678,51 @@ def test_captured_forward_hipgraph(gpu_device):
         t.mul_(0.5)
     again = cap.replay()
     assert torch.equal(again, engine.propagate_forward(g, segs, K))
+
+
+def test_featsplit_training_step_matches_single_gpu(gpu_device):
+    """One main.py training step (main.py:488-531) through the featsplit path (one rank: the
+    slot-space shard, _ShardPropagate with the engine backward on the relabelled transpose,
+    the sharded BPR loss) == the drop-in model's step: same loss, same gradients (1e-5)."""
+    import socket
+    import torch.distributed as dist
+    from gcn_recommendation_amd import dist as D
+    from conftest import ROOT  # noqa: F401
+    own = not dist.is_initialized()
+    if own:
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+        s_.close()
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1)
+    try:
+        z = load_case("c1_nobrand")
+        U, I, B, d, K = case_dims(z)
+        n = U + I + B
+        m = _model(z, gpu_device)
+        adj = _adj(z, gpu_device)
+        bu, bp, bn = (torch.from_numpy(z[k]).to(gpu_device) for k in ("bpr_users", "bpr_pos",
+                                                                      "bpr_neg"))
+        fu, fi, fb, u0, i0 = m(adj, use_brand=False)
+        ref = bpr_loss_reg(fu[bu], fi[bp], fi[bn], u0[bu], i0[bp], i0[bn], 1e-4)
+        ref.backward()
+        r, c, v = z["adj_row"].astype(np.int64), z["adj_col"].astype(np.int64), z["adj_val"]
+        rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
+        plan = D.FeatSplitPlan(rowptr, c, v, n, gpu_device).attach_transpose(rowptr, c, v)
+        segs = [p.detach() for p in (m.user_embedding.weight, m.item_embedding.weight,
+                                     m.brand_embedding.weight)]
+        x, _ = plan.shard(segs, 1, 0)
+        w = torch.nn.Parameter(x)
+        out = D._ShardPropagate.apply(plan, K, engine.hub_threshold_from_env(), w)
+        su, sp, sn = plan.slots(bu), plan.slots(U + bp), plan.slots(U + bn)
+        loss = D.bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
+        loss.backward()
+        assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item())
+        g = plan.unshard(w.grad).cpu().numpy()
+        assert_close_normwise(g[:U], m.user_embedding.weight.grad.cpu().numpy(), what="d user")
+        assert_close_normwise(g[U:U + I], m.item_embedding.weight.grad.cpu().numpy(),
+                              what="d item")
+    finally:
+        if own:
+            dist.destroy_process_group()
