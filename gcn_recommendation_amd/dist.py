@@ -386,7 +386,7 @@ def featsplit_backward_timing(plan, rowptr, c, v, x_slot, K, args, dev, hub_thr)
     return out
 
 
-class _ShardPropagate(torch.autograd.Function):
+class ShardPropagate(torch.autograd.Function):
     """A featsplit rank's forward (its columns, slot space) with the engine backward."""
 
     @staticmethod
@@ -416,7 +416,7 @@ def featsplit_train_timing(plan, x_slot, K, args, dev, hub_thr, batch=2048):
     def step(timed):
         su, sp, sn = next(it)
         opt.zero_grad()
-        out = _ShardPropagate.apply(plan, K, hub_thr, w)
+        out = ShardPropagate.apply(plan, K, hub_thr, w)
         loss = bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
         loss.backward()
         opt.step()

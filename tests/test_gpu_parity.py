@@ -682,7 +682,7 @@ def test_captured_forward_hipgraph(gpu_device):
 
 def test_featsplit_training_step_matches_single_gpu(gpu_device):
     """One main.py training step (main.py:488-531) through the featsplit path (one rank: the
-    slot-space shard, _ShardPropagate with the engine backward on the relabelled transpose,
+    slot-space shard, ShardPropagate with the engine backward on the relabelled transpose,
     the sharded BPR loss) == the drop-in model's step: same loss, same gradients (1e-5)."""
     import socket
     import torch.distributed as dist
@@ -714,7 +714,7 @@ def test_featsplit_training_step_matches_single_gpu(gpu_device):
                                      m.brand_embedding.weight)]
         x, _ = plan.shard(segs, 1, 0)
         w = torch.nn.Parameter(x)
-        out = D._ShardPropagate.apply(plan, K, engine.hub_threshold_from_env(), w)
+        out = D.ShardPropagate.apply(plan, K, engine.hub_threshold_from_env(), w)
         su, sp, sn = plan.slots(bu), plan.slots(U + bp), plan.slots(U + bn)
         loss = D.bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
         loss.backward()
