@@ -8,7 +8,6 @@ the reference expression, written out with torch ops (training only): g = dF whe
 slope * dF; d_id = g · W[:, :d]; dW = gᵀ · [id | content]; db = Σ g. The content table is a
 buffer (no gradient), as in the reference.
 """
-import ctypes
 
 import torch
 
