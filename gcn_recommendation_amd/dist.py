@@ -458,6 +458,26 @@ def featsplit_c4(plan, world, rank, nnz, n, args, dev, hub_thr):
             "store_layer_ms": round(store_ms, 4)}
 
 
+def profiled_traffic(cfg, args, mode, d_rank):
+    """HBM bytes per launch of a featsplit rank's STORE layer at this column width, from the
+    committed PMC profiles (profiles/traffic_c3_featsplit_*.json; C3 power-law only), or None."""
+    if mode != "featsplit" or cfg.get("name", "").split()[0] != "C3" or args.gen != "powerlaw":
+        return None
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+    import json
+    try:
+        if d_rank == 8:
+            return json.load(open(os.path.join(root, "traffic_c3_featsplit_d8.json")))[
+                "hbm_bytes_per_launch"]
+        if d_rank in (16, 32):
+            ks = json.load(open(os.path.join(root, "traffic_c3_featsplit_d16_d32.json")))["kernels"]
+            return int(next(v["hbm_bytes_per_launch"] for k, v in ks.items()
+                            if k.startswith(f"d={d_rank} STORE")))
+    except (OSError, KeyError, StopIteration, ValueError):
+        return None
+    return None
+
+
 def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     rank, world = init("cuda")
     d, K = cfg["d"], cfg["K"]
@@ -522,7 +542,9 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
                    "hub_threshold": hub_thr, "parallelism": f"{mode}{world}",
                    "exchange_bytes_per_step_per_rank": int(comm), **extra},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
-                     "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / 8000.0, 4),
+                     "traffic": profiled_traffic(cfg, args, mode, d // world if mode == "featsplit"
+                                                 else None),
                      "kernel": "k_layer store layers, per GPU (max over ranks)",
                      "bytes_per_launch": int(b_layer), "avg_launch_ms": round(kern_ms, 4)},
         **({"backward": bwd} if bwd else {}),
