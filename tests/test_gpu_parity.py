@@ -274,6 +274,17 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, thr):
                                      P(work), P(ge0), st)
     assert rc == 0
     assert torch.equal(ge0, engine.propagate_backward(g, [G], K, thr, sparse="off"))
+    # row-sparse upstream gradient through the C entry point's grad_nz path
+    Gs = torch.zeros_like(G)
+    live = torch.arange(0, n, 97, device=gpu_device)
+    Gs[live] = G[live]
+    nz, _ = engine.rows_nonzero([Gs], d, gpu_device)
+    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n, thr,
+                                     P(hpt.items), hpt.n_items, P(hpt.rows), hpt.n_entries,
+                                     hpt.n_pre, P(part_t), engine.rows_desc([Gs], d), P(nz), d, K,
+                                     P(work), P(ge0), st)
+    assert rc == 0
+    assert torch.equal(ge0, engine.propagate_backward(g, [Gs], K, thr, sparse="off"))
 
 
 def test_segments_and_misaligned_rows(gpu_device):
