@@ -96,6 +96,15 @@ __device__ __forceinline__ const float* seg_row(const lgcn_rows_t& s, int32_t r)
 #endif
 typedef float f4_t __attribute__((ext_vector_type(4)));
 
+// MEAN bundle prefetch: widest lane group it is used for (8: d <= 32; 16 adds d = 64 with
+// bundles of LGCN_MEAN_PF_RPG16 rows) — build-time A/B knobs
+#ifndef LGCN_MEAN_PF_MAX_G
+#define LGCN_MEAN_PF_MAX_G 8
+#endif
+#ifndef LGCN_MEAN_PF_RPG16
+#define LGCN_MEAN_PF_RPG16 4
+#endif
+
 __device__ __forceinline__ int2 load_edge(const lgcn_edge_t* e) {
     if constexpr (LGCN_NT & 1) {
         const long long v = __builtin_nontemporal_load(reinterpret_cast<const long long*>(e));
@@ -755,10 +764,10 @@ int launch_layer_t(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_
         }
         return launch_layer_rpg<V, G, NV, MODE, XD, 1, U1>(LGCN_ARGS);
     }
-    if constexpr (MODE == LGCN_EPI_MEAN && NV == 1 && G >= 4 && G <= 8) {
+    if constexpr (MODE == LGCN_EPI_MEAN && NV == 1 && G >= 4 && G <= LGCN_MEAN_PF_MAX_G) {
         // small d (featsplit shards): the flush's E0..E_{K-1} row reads are latency on the
         // critical path; bundles of RM rows prefetch them (RM register slots per layer)
-        constexpr int RM = G >= 8 ? 4 : RB;
+        constexpr int RM = G >= 16 ? LGCN_MEAN_PF_RPG16 : G >= 8 ? 4 : RB;
         if (lgcn_detail::g_mean_prefetch != 2 && per >= RM && (dW & (dW - 1)) == 0) {
             if (ep.n_prev == 2) return launch_layer_rpg<V, G, NV, MODE, XD, RM, UB, 2>(LGCN_ARGS);
             if (ep.n_prev == 3) return launch_layer_rpg<V, G, NV, MODE, XD, RM, UB, 3>(LGCN_ARGS);
