@@ -12,7 +12,7 @@ CSRC = os.path.join(_PKG, "csrc")
 SRCS = [os.path.join(CSRC, f) for f in (
     "lgcn_layer_add_sparse.hip", "lgcn_layer_add_div.hip", "lgcn_layer_add.hip",
     "lgcn_layer_mean.hip", "lgcn_layer_store.hip", "lgcn_engine.hip", "lgcn_eval.hip",
-    "lgcn_bpr.hip", "lgcn_fusion.hip")]
+    "lgcn_bpr.hip", "lgcn_fusion.hip", "lgcn_exact.hip")]
 HDRS = [os.path.join(ROOT, "include", "lgcn.h"), os.path.join(CSRC, "lgcn_kernels.h")]
 OUT = os.path.join(_PKG, "liblgcn_engine.so")
 OBJ_DIR = os.path.join(_PKG, "_obj")

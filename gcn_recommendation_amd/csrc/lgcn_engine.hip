@@ -637,11 +637,55 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
     return scale_rows(x, n_rows, d, div, y, ldy, S(stream));
 }
 
+// one layer under a hub plan: emulation block pass -> bundles/chunks/long rows -> combine -> walk
+static int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                      int32_t n, const lgcn_hub_plan_t& p, const lgcn_rows_t& x, float xdiv,
+                      const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
+                      const lgcn_epilogue_t& ep, hipStream_t s) {
+    if (p.n_emu_rows > 0) {
+        if (int e = lgcn_emu_blocks(edges, p.emu_blocks, p.n_emu_blocks, x, xdiv, x_nz, d,
+                                    p.emu_rel, p.emu_meta, p.emu_stage, s))
+            return e;
+    }
+    if (int e = spmm_layer(rowptr, edges, row_ids, n, p.threshold, p.items, p.n_items, p.partials,
+                           x, y, ldy, d, ep, xdiv, x_nz, s))
+        return e;
+    if (int e = hub_combine(p.rows, p.n_rows, p.n_pre, p.partials, y, ldy, d, ep, s)) return e;
+    if (p.n_emu_rows > 0) {
+        if (int e = lgcn_emu_walk(edges, p.emu_blocks, p.emu_rows, p.n_emu_rows, p.emu_rel,
+                                  p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, s))
+            return e;
+    }
+    return 0;
+}
+
+static int check_plan(const lgcn_hub_plan_t* p) {
+    if (!p) return LGCN_EINVAL;
+    if (p->n_items < 0 || (p->n_items > 0 && !p->items)) return LGCN_EINVAL;
+    if (p->n_rows < 0 || p->n_pre < 0 || p->n_pre > p->n_rows) return LGCN_EINVAL;
+    if (p->n_rows > 0 && (!p->rows || !p->partials)) return LGCN_EINVAL;
+    if (p->n_emu_rows < 0 || p->n_emu_blocks < 0) return LGCN_EINVAL;
+    if (p->n_emu_rows > 0 && (!p->emu_rows || !p->emu_blocks || !p->emu_rel || !p->emu_meta))
+        return LGCN_EINVAL;
+    return 0;
+}
+
+int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+               int32_t n_rows, const lgcn_hub_plan_t* plan, lgcn_rows_t x, float x_div,
+               const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
+               const lgcn_epilogue_t* epi_host, void* stream) {
+    if (int e = valid_geom(n_rows, d)) return e;
+    if (int e = check_epi(epi_host)) return e;
+    if (int e = check_plan(plan)) return e;
+    if (n_rows > 0 && (!rowptr || !y || ldy < d)) return LGCN_EINVAL;
+    if (!(x_div > 0.f)) return LGCN_EINVAL;
+    if (epi_host->mode != LGCN_EPI_ADD && (x_div != 1.f || x_nz)) return LGCN_EINVAL;
+    return plan_layer(rowptr, edges, row_ids, n_rows, *plan, x, x_div, x_nz, y, ldy, d,
+                      *epi_host, S(stream));
+}
+
 int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
-                           const int32_t* row_ids, int32_t n,
-                           int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
-                           int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                           int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                           const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                            lgcn_rows_t emb, int32_t d,
                            int32_t K, float* const* layer_bufs_host, float* out,
                            void* const* ev_host, void* stream) {
@@ -650,6 +694,7 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
     if (K > 1 && !layer_bufs_host) return LGCN_EINVAL;
     hipStream_t s = S(stream);
     if (K == 0) return scale_rows(emb, n, d, 1.0f, out, d, s);
+    if (int e = check_plan(plan)) return e;
     for (int k = 1; k <= K; ++k) {
         const lgcn_rows_t x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
         lgcn_epilogue_t ep;
@@ -670,23 +715,17 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1)], s))) return e;
         }
-        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items,
-                               partials, x, y, d, d, ep, 1.f, nullptr, s))
+        if (int e = plan_layer(rowptr, edges, row_ids, n, *plan, x, 1.f, nullptr, y, d, d, ep, s))
             return e;
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1) + 1], s))) return e;
         }
-        if (int e = hub_combine(hub_rows, n_hub_rows, n_pre_rows, partials, y, d, d, ep, s))
-            return e;
     }
     return 0;
 }
 
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
-                            const int32_t* row_ids, int32_t n,
-                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
-                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                            const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                             lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                             float* grad_e0, void* stream) {
@@ -695,6 +734,7 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
     hipStream_t s = S(stream);
     if (K == 0) return scale_rows(grad_out, n, d, 1.0f, grad_e0, d, s);
     if (K > 1 && !work_h) return LGCN_EINVAL;
+    if (int e = check_plan(plan)) return e;
     // MeanBackward hands every layer c = G / (K+1); it is never materialised: layer 1 gathers
     // G / (K+1) on load and every epilogue adds G[row] / (K+1) (same rounding as c).
     const float div = (float)(K + 1);
@@ -709,10 +749,7 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
     const uint32_t* x_nz = grad_nz;
     for (int k = 1; k <= K; ++k) {
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
-        if (int e = spmm_layer(rowptr, edges, row_ids, n, hub_threshold, hub_items, n_hub_items,
-                               partials, h, y, d, d, ep, xdiv, x_nz, s))
-            return e;
-        if (int e = hub_combine(hub_rows, n_hub_rows, n_pre_rows, partials, y, d, d, ep, s))
+        if (int e = plan_layer(rowptr, edges, row_ids, n, *plan, h, xdiv, x_nz, y, d, d, ep, s))
             return e;
         h = dense_rows(y, n, d);
         xdiv = 1.f;

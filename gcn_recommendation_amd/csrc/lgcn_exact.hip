@@ -1,0 +1,593 @@
+// lgcn_exact.hip — hub rows summed with the reference's exact arithmetic at any degree.
+//
+// The reference (models/lightgcn.py:45, torch.sparse.mm -> ATen addmm_sparse_dense_cpu) folds
+// every row of Â·X as ONE sequential chain acc = fma(val_j, X[col_j, c], acc) per column c, in
+// stored edge order, from +0. On a power-law graph one item row holds millions of edges; a chain
+// that long is millions of dependent FMAs (~4.6 ms per layer for the 2.77M-edge row of the
+// Books-scale graph even at one FMA per 4 cycles). This file reproduces that chain bit for bit
+// without running it step by step.
+//
+// Translation invariance. Let e be a binade (|a| in [2^e, 2^(e+1))) and u = 2^(e-23) its ulp.
+// If a chain value a is a multiple of u and a + p stays inside binade e, then
+// fma-rounding gives RN(a + p) = a + RN_u(p) (RN_u: nearest multiple of u; the tie case depends
+// on a's parity). So two chains over the same steps, started from a and a' in binade e, stay
+// exactly a - a' apart as long as both trajectories stay inside the binade (and no step is an
+// exact tie). Hence:
+//   * k_emu_blocks cuts a hub row into blocks of <= 256 edges. For each (block, column) it runs
+//     32 CANDIDATE chains from a' = +-1.5 * 2^e, e in a 16-binade window chosen from the block's
+//     own first products, and records rel = chain_end - a' (exact), bounds lo/hi on the exact
+//     running sum of its products (from the block's own chain from +0, widened by its rounding
+//     error; every trajectory of the block stays within 128 ulps of that sum), and the largest
+//     lowest-set-bit exponent of its products (a product can be an exact tie only if that
+//     exponent reaches e - 24). Block 0 of a row keeps its chain from +0: the true value.
+//   * k_emu_walk (one wave per (row, column)) walks the blocks in order with the true value a:
+//     if a's binade has a candidate, both trajectories provably stay inside it and no tie is
+//     possible, a += rel (exact); otherwise the block is re-run as the sequential fma chain.
+// Every step is therefore either the reference's own fma or a proven-identical translation:
+// the result is bitwise the reference's, whatever the data (ties, zero crossings, subnormals,
+// inf/NaN all take the sequential path). oracle/lgcn_oracle.c holds the sequential chain the
+// tests compare against; DESIGN.md §3 has the argument and the measured slow-block fractions.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "lgcn.h"
+
+namespace {
+
+constexpr int kW = LGCN_EMU_CANDS / 2;  // binades per sign
+constexpr int kEOff = 2;                // window starts 2 binades above the first 64 steps' reach
+constexpr int16_t kIdentity = -32768;   // maxlsb sentinel: no nonzero product in the block
+constexpr int16_t kNoFast = 32000;      // maxlsb sentinel: never take the fast path
+constexpr int kSlack = 132;             // ulps: 128 for <= 256 steps of <= 1/2 ulp + margin
+
+struct EmuMeta {
+    int32_t lo;      // floor(L * 2^(23 - ebase)), L a lower bound of the block's exact running sum
+    int32_t hi;      // ceil(H * 2^(23 - ebase)), H an upper bound
+    int16_t ebase;   // binade of candidate pair 0
+    int16_t maxlsb;  // max over nonzero products of the exponent of their lowest set bit
+                     // (kIdentity: no nonzero product; kNoFast: bounds too wide for int32)
+    float r0;        // block 0 of a row: the exact chain from +0
+};
+static_assert(sizeof(EmuMeta) == LGCN_EMU_META_BYTES, "meta record size");
+
+__device__ __forceinline__ const float* seg_row_x(const lgcn_rows_t& s, int32_t r) {
+    if (r < s.end0) return s.p0 + (int64_t)r * s.ld;
+    if (r < s.end1) return s.p1 + (int64_t)(r - s.end0) * s.ld;
+    return s.p2 + (int64_t)(r - s.end1) * s.ld;
+}
+
+__device__ __forceinline__ bool row_live_x(const uint32_t* __restrict__ nz, int32_t r) {
+    return (nz[r >> 5] >> (r & 31)) & 1u;
+}
+
+// X element as the layer kernels read it (lgcn_kernels.h load_x): XD & 3 = 1: / xdiv (IEEE),
+// 2: * xdiv (host passes the exact reciprocal of a power-of-two divisor); XD & 4: row-sparse X
+// (dead rows are all zero: fma(v, +-0, acc) == acc for every value a chain holds).
+// Branch-free: the segment is chosen by selects and every load is issued unconditionally at a
+// valid address (`ok` masks the value), so a batch of these loads is all in flight at once.
+__device__ __forceinline__ const float* seg_row_sel(const lgcn_rows_t& s, int32_t r) {
+    // p0 + an integer offset: a per-lane select between the three base POINTERS is turned by
+    // the compiler into a per-lane load from the kernel-argument segment (a dependent round
+    // trip before the element load); selecting between integer deltas keeps it in registers
+    const char* b = reinterpret_cast<const char*>(s.p0);
+    const int64_t row_b = s.ld * 4;
+    const int64_t d1 = (reinterpret_cast<const char*>(s.p1) - b) - (int64_t)s.end0 * row_b;
+    const int64_t d2 = (reinterpret_cast<const char*>(s.p2) - b) - (int64_t)s.end1 * row_b;
+    const int64_t off = (int64_t)r * row_b + (r < s.end0 ? 0 : (r < s.end1 ? d1 : d2));
+    return reinterpret_cast<const float*>(b + off);
+}
+
+template <int XD>
+__device__ __forceinline__ float load_elem(const lgcn_rows_t& x, const uint32_t* x_nz, int32_t col,
+                                           int c, float xdiv, bool ok = true) {
+    // uniform row base + a 32-bit lane offset (global_load ... saddr form)
+    float v = *reinterpret_cast<const float*>(
+        reinterpret_cast<const char*>(seg_row_sel(x, col)) + (uint32_t)c * 4u);
+    if constexpr ((XD & 4) != 0) ok = ok && row_live_x(x_nz, col);
+    v = ok ? v : 0.f;
+    if constexpr ((XD & 3) == 1) return v / xdiv;
+    else if constexpr ((XD & 3) == 2) return v * xdiv;
+    else return v;
+}
+
+// exponent of the lowest set bit of a finite nonzero float (subnormals included)
+__device__ __forceinline__ int lsb_exp(float f) {
+    const uint32_t b = __float_as_uint(f);
+    const int E = (int)((b >> 23) & 255u);
+    const uint32_t M = b & 0x7fffffu;
+    if (E == 0) return -149 + __builtin_ctz(M);
+    return E - 150 + __builtin_ctz(M | 0x800000u);
+}
+
+// ---------------------------------------------------------------------------------------------
+// block pass: one wave per (block, 64-column slice); lane = column
+// ---------------------------------------------------------------------------------------------
+template <int XD>
+__global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict__ edges,
+                                                   const lgcn_emu_block_t* __restrict__ blocks,
+                                                   lgcn_rows_t x, float xdiv,
+                                                   const uint32_t* __restrict__ x_nz, int32_t d,
+                                                   int32_t* __restrict__ rel,
+                                                   EmuMeta* __restrict__ meta,
+                                                   float* __restrict__ stage) {
+    constexpr int SW = 16;  // steps gathered per sub-window (all in flight at once)
+    const int lane = threadIdx.x;
+    const int c = blockIdx.y * 64 + lane;
+    const bool act = c < d;
+    const lgcn_emu_block_t blk = blocks[blockIdx.x];
+    // T: the sequential fma chain of the block from +0. It is the true chain for block 0; for
+    // every block it tracks the exact running sum S of the products to within 1/2 ulp(|T|) per
+    // step, which bounds every trajectory of the block (EmuMeta lo/hi)
+    float T = 0.f, tlo = 0.f, thi = 0.f;
+    int maxlsb = -100000;
+    float cand[LGCN_EMU_CANDS];
+    bool init = false;
+    int ebase = 0;
+    const int cc = act ? c : d - 1;  // lanes past d load a valid element and mask it
+    // lane l holds edge record j0 + l of the current 64-edge window ((0, 0) past the block)
+    auto load_rec = [&](int32_t j0) {
+        const int32_t j = min(j0 + lane, blk.end - 1);
+        const int2 r = *reinterpret_cast<const int2*>(edges + j);
+        return j0 + lane < blk.end ? r : make_int2(0, 0);
+    };
+    auto load_sub = [&](const int2& rec, int s0, int n, float (&xv)[SW], float (&vv)[SW]) {
+#pragma unroll
+        for (int t = 0; t < SW; ++t) {
+            const int32_t col = __builtin_amdgcn_readlane(rec.x, s0 + t);
+            vv[t] = __int_as_float(__builtin_amdgcn_readlane(rec.y, s0 + t));
+            xv[t] = load_elem<XD>(x, x_nz, col, cc, xdiv, act && s0 + t < n);
+        }
+    };
+    // one sub-window: steps past the block end read as (0, 0), and fma(0, 0, c) == c for every
+    // chain value (a chain is never -0), so the unrolled steps need no guard
+    // this (block, column)'s elements, in step order (the walk re-runs a block from here)
+    float* st = stage ? stage + ((int64_t)blockIdx.x * d + cc) * LGCN_EMU_BLOCK : nullptr;
+    auto stage_sub = [&](const float (&xv)[SW], int step0) {
+        if (!st || !act) return;
+#pragma unroll
+        for (int q = 0; q < SW / 4; ++q)
+            *reinterpret_cast<float4*>(st + step0 + 4 * q) =
+                make_float4(xv[4 * q], xv[4 * q + 1], xv[4 * q + 2], xv[4 * q + 3]);
+    };
+    auto run_sub = [&](const float (&xv)[SW], const float (&vv)[SW]) {
+        if (!init) {
+            // candidates start at the first sub-window holding a nonzero product (before it the
+            // block is the identity for every start value); their binade window starts kEOff
+            // above this sub-window's reach
+            float s = T, m = 0.f;
+#pragma unroll
+            for (int t = 0; t < SW; ++t) {
+                s = __builtin_fmaf(vv[t], xv[t], s);
+                m = fmaxf(m, fabsf(s));
+            }
+            if (m > 0.f && m <= 3.0e38f) {
+                init = true;
+                int e;
+                frexpf(m, &e);
+                ebase = max(-200, min(e - 1 + kEOff + 1, 200));  // 16 steps reach ~1/2 of 64
+#pragma unroll
+                for (int k = 0; k < LGCN_EMU_CANDS; ++k) {
+                    const int eb = ebase + (k >> 1);
+                    const float a0 = (eb >= -126 && eb <= 127) ? ldexpf(1.5f, eb) : 1.5f;
+                    cand[k] = (k & 1) ? -a0 : a0;
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < SW; ++t) {
+            T = __builtin_fmaf(vv[t], xv[t], T);
+            tlo = fminf(tlo, T);
+            thi = fmaxf(thi, T);
+            const int le = lsb_exp(vv[t]) + lsb_exp(xv[t]);
+            maxlsb = (vv[t] != 0.f && xv[t] != 0.f) ? max(maxlsb, le) : maxlsb;
+        }
+        if (init) {
+#pragma unroll
+            for (int t = 0; t < SW; ++t) {
+#pragma unroll
+                for (int k = 0; k < LGCN_EMU_CANDS; ++k)
+                    cand[k] = __builtin_fmaf(vv[t], xv[t], cand[k]);
+            }
+        }
+    };
+    int2 rec = load_rec(blk.beg);
+    for (int32_t j0 = blk.beg; j0 < blk.end; j0 += 64) {
+        const int n = min(64, blk.end - j0);
+        const int2 nrec = load_rec(j0 + 64);  // next window's records, in flight meanwhile
+        float xa[SW], va[SW], xb[SW], vb[SW];
+        // the loads of sub-window k + 1 are issued before sub-window k is computed
+        const int w0 = j0 - blk.beg;
+        load_sub(rec, 0, n, xa, va);
+        load_sub(rec, 16, n, xb, vb);
+        run_sub(xa, va);
+        stage_sub(xa, w0);
+        load_sub(rec, 32, n, xa, va);
+        run_sub(xb, vb);
+        stage_sub(xb, w0 + 16);
+        load_sub(rec, 48, n, xb, vb);
+        run_sub(xa, va);
+        stage_sub(xa, w0 + 32);
+        run_sub(xb, vb);
+        stage_sub(xb, w0 + 48);
+        rec = nrec;
+    }
+    if (!act) return;
+    const int64_t rc = (int64_t)blockIdx.x * d + c;
+    // candidate k's translation in units of its ulp u_k = 2^(ebase + k/2 - 23): exact integer
+    // when the candidate's chain stayed in its binade (the walker checks exactly that)
+    int4* rp = reinterpret_cast<int4*>(rel + rc * LGCN_EMU_CANDS);
+#pragma unroll
+    for (int q = 0; q < LGCN_EMU_CANDS / 4; ++q) {
+        int r4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int k = 4 * q + t;
+            const int eb = ebase + (k >> 1);
+            const float a0 = (eb >= -126 && eb <= 127) ? ldexpf(1.5f, eb) : 1.5f;
+            const float dlt = cand[k] - ((k & 1) ? -a0 : a0);
+            const float ku = ldexpf(dlt, 23 - eb);
+            r4[t] = (init && fabsf(ku) < 16777216.f) ? (int)ku : 0;
+        }
+        rp[q] = make_int4(r4[0], r4[1], r4[2], r4[3]);
+    }
+    // |T_j - S_j| <= j * ulp(max|T|) / 2 <= 128 * ulp(max|T|) for a block of <= 256 steps
+    const float M = fmaxf(-tlo, thi);
+    double err = 0.0;
+    if (M > 0.f) {
+        int e;
+        frexpf(M, &e);  // M in [2^(e-1), 2^e): ulp(M) <= 2^(e-24) (subnormal ulp: 2^-149)
+        err = (LGCN_EMU_BLOCK / 2) * ldexp(1.0, max(e - 24, -149));
+    }
+    const double lo_u = floor(ldexp((double)tlo - err, 23 - ebase));
+    const double hi_u = ceil(ldexp((double)thi + err, 23 - ebase));
+    const bool fits = lo_u >= -1073741824.0 && hi_u <= 1073741824.0;
+    EmuMeta m;
+    m.lo = fits ? (int32_t)lo_u : 0;
+    m.hi = fits ? (int32_t)hi_u : 0;
+    m.ebase = (int16_t)ebase;
+    m.maxlsb = (maxlsb == -100000) ? kIdentity
+               : !fits ? kNoFast : (int16_t)max(-32000, min(maxlsb, 31999));
+    m.r0 = T;
+    meta[rc] = m;
+}
+
+// ---------------------------------------------------------------------------------------------
+// walker: one wave per (hub row, column). The chain value is wave-uniform.
+// ---------------------------------------------------------------------------------------------
+// The block's steps as the reference runs them: a = fma(val_j, x_j, a) in stored order. All
+// (val, x) pairs are fetched at once (<= 4 per lane, one round trip) into LDS, then every lane
+// runs the same chain (the result is wave-uniform).
+template <int XD>
+__device__ float emu_slow_block(const lgcn_edge_t* __restrict__ edges, int32_t beg, int32_t end,
+                                const lgcn_rows_t& x, float xdiv, const uint32_t* __restrict__ x_nz,
+                                const float* __restrict__ st, int c, float a, float2* sq) {
+    const int lane = threadIdx.x;
+    const int n = end - beg;
+    constexpr int Q = LGCN_EMU_BLOCK / 64;
+    int2 rec[Q];
+#pragma unroll
+    for (int t = 0; t < Q; ++t)  // every record load in flight at once (clamped, masked below)
+        rec[t] = *reinterpret_cast<const int2*>(edges + beg + min(t * 64 + lane, n - 1));
+    float2 q[Q];
+    if (st) {  // the block pass staged this column's elements: contiguous, no dependent gather
+        const float4 xs = *reinterpret_cast<const float4*>(st + 4 * lane);
+        const float xv[4] = {xs.x, xs.y, xs.z, xs.w};
+        // step 4 * lane + t  ->  LDS slot; written below in (t * 64 + lane) order, so first
+        // exchange through LDS
+#pragma unroll
+        for (int t = 0; t < Q; ++t) {
+            const bool in = t * 64 + lane < n;
+            q[t] = make_float2(in ? __int_as_float(rec[t].y) : 0.f, 0.f);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < Q; ++t) sq[t * 64 + lane] = q[t];
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (4 * lane + t < n) sq[4 * lane + t].y = xv[t];
+        __syncthreads();
+    } else {
+#pragma unroll
+        for (int t = 0; t < Q; ++t) {  // then every element load
+            const bool in = t * 64 + lane < n;
+            q[t] = make_float2(in ? __int_as_float(rec[t].y) : 0.f,
+                               load_elem<XD>(x, x_nz, rec[t].x, c, xdiv, in));
+        }
+    }
+    if (!st) {
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < LGCN_EMU_BLOCK / 64; ++t) sq[t * 64 + lane] = q[t];
+        __syncthreads();
+    }
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        float2 w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = sq[i + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a = __builtin_fmaf(w[k].x, w[k].y, a);
+    }
+    for (; i < n; ++i) a = __builtin_fmaf(sq[i].x, sq[i].y, a);
+    return a;
+}
+
+// LGCN_EMU_STATS builds (diagnostics only, tools/exact_probe.py): walker decision counters
+// [fast, slow, identity, slow: zero/subnormal, slow: window, slow: tie, slow: bounds, slow steps]
+#ifdef LGCN_EMU_STATS
+__device__ unsigned long long g_emu_stats[8];
+// per emulated row (first 256 rows): fast blocks, slow blocks, cycles in slow blocks, max cycles
+__device__ unsigned long long g_emu_row_stats[256][4];
+#define EMU_STAT(k, v) \
+    do { if (threadIdx.x == 0) atomicAdd(&g_emu_stats[k], (unsigned long long)(v)); } while (0)
+#else
+#define EMU_STAT(k, v) ((void)0)
+#endif
+
+// Fast-path test for one block on the chain value's bits ab (wave-uniform integer arithmetic):
+// true if the block maps ab to ab +- K[*idx] exactly. With e = binade(a), u = 2^(e-23), M = the
+// integer mantissa (a = +-M u, 2^23 <= M < 2^24) and [lo, hi] the block's bounds in units of u,
+// every trajectory value c_j = a + (c_j - a) stays in [2^e + u, 2^(e+1) - u] iff its mantissa
+// stays in [2^23 + 1, 2^24 - 1]; kSlack covers the per-step rounding drift.
+__device__ __forceinline__ bool emu_fast(uint32_t ab, int32_t lo0, int32_t hi0, int ebase,
+                                         int maxlsb, int* idx) {
+    const int E = (int)((ab >> 23) & 255u);
+    if (E == 0 || E == 255) {  // zero / subnormal / inf / NaN: sequential
+        EMU_STAT(3, 1);
+        return false;
+    }
+    const int w = E - 127 - ebase;
+    if (w < 0 || w >= kW) {
+        EMU_STAT(4, 1);
+        return false;
+    }
+    if (maxlsb >= E - 127 - 24) {  // a product may be an exact tie in this binade
+        EMU_STAT(5, 1);
+        return false;
+    }
+    const int lo = lo0 >> w;        // floor(lo0 / 2^w)
+    const int hi = -((-hi0) >> w);  // ceil(hi0 / 2^w)
+    const int M = (int)((ab & 0x7fffffu) | 0x800000u);
+    constexpr int LB = (1 << 23) + kSlack, HB = (1 << 24) - kSlack, C = 3 << 22;  // C: 1.5 * 2^23
+    const bool neg = (ab >> 31) != 0;
+    bool ok;
+    if (!neg) ok = M + lo >= LB && M + hi <= HB && C + lo >= LB && C + hi <= HB;
+    else ok = M - hi >= LB && M - lo <= HB && C - hi >= LB && C - lo <= HB;
+    *idx = 2 * w + (neg ? 1 : 0);
+    if (!ok) EMU_STAT(6, 1);
+    return ok;
+}
+
+template <int MODE, int XD>
+__global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__ edges,
+                                                 const lgcn_emu_block_t* __restrict__ blocks,
+                                                 const lgcn_emu_row_t* __restrict__ rows,
+                                                 const int32_t* __restrict__ rel,
+                                                 const EmuMeta* __restrict__ meta,
+                                                 const float* __restrict__ stage, lgcn_rows_t x,
+                                                 float xdiv, const uint32_t* __restrict__ x_nz,
+                                                 int32_t d, float* __restrict__ y, int64_t ldy,
+                                                 lgcn_epilogue_t ep) {
+    constexpr int CH = 64;  // blocks staged per chunk
+    __shared__ int32_t srel[CH * LGCN_EMU_CANDS];
+    __shared__ float2 sq[LGCN_EMU_BLOCK];
+    const int lane = threadIdx.x;
+    const int c = blockIdx.y;
+    const lgcn_emu_row_t er = rows[blockIdx.x];
+    // the chain value, as its bits (wave-uniform)
+    uint32_t ab = __float_as_uint(meta[(int64_t)er.first_block * d + c].r0);
+#ifdef LGCN_EMU_STATS
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long n_fast = 0, n_slow = 0, t_slow = 0;
+#endif
+    for (int32_t b0 = 1; b0 < er.n_blocks; b0 += CH) {
+        const int nb = min(CH, er.n_blocks - b0);
+        // stage the chunk: lane i holds block b0+i's meta; srel[i][k] its translations
+        int32_t mlo = 0, mhi = 0, mpk = 0;
+        __syncthreads();
+        if (lane < nb) {
+            const int64_t rc = (int64_t)(er.first_block + b0 + lane) * d + c;
+            const int4 mv = *reinterpret_cast<const int4*>(meta + rc);
+            mlo = mv.x;
+            mhi = mv.y;
+            mpk = mv.z;
+            const int4* rp = reinterpret_cast<const int4*>(rel + rc * LGCN_EMU_CANDS);
+            int4* dst = reinterpret_cast<int4*>(srel + lane * LGCN_EMU_CANDS);
+#pragma unroll
+            for (int q = 0; q < LGCN_EMU_CANDS / 4; ++q) dst[q] = rp[q];
+        }
+        __syncthreads();
+        // lane k (< 32) holds the current block's translation k, read one block ahead
+        int32_t kv = srel[lane & (LGCN_EMU_CANDS - 1)];
+        for (int i = 0; i < nb; ++i) {
+            const int32_t lo0 = __builtin_amdgcn_readlane(mlo, i);
+            const int32_t hi0 = __builtin_amdgcn_readlane(mhi, i);
+            const int32_t pk = __builtin_amdgcn_readlane(mpk, i);
+            const int32_t kcur = kv;
+            if (i + 1 < nb) kv = srel[(i + 1) * LGCN_EMU_CANDS + (lane & (LGCN_EMU_CANDS - 1))];
+            const int ebase = (int)(int16_t)(pk & 0xffff);
+            const int maxlsb = (int)(int16_t)(pk >> 16);
+            if (maxlsb == kIdentity) {  // every product is zero: a is unchanged
+                EMU_STAT(2, 1);
+                continue;
+            }
+            int idx = 0;
+            if (emu_fast(ab, lo0, hi0, ebase, maxlsb, &idx)) {
+                EMU_STAT(0, 1);
+#ifdef LGCN_EMU_STATS
+                ++n_fast;
+#endif
+                const int32_t K = __builtin_amdgcn_readlane(kcur, idx);
+                ab = (ab >> 31) ? ab - (uint32_t)K : ab + (uint32_t)K;  // same binade: mantissa add
+            } else {
+                const lgcn_emu_block_t bk = blocks[er.first_block + b0 + i];
+                EMU_STAT(1, 1);
+                EMU_STAT(7, bk.end - bk.beg);
+#ifdef LGCN_EMU_STATS
+                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+                const int64_t bi = er.first_block + b0 + i;
+                const float* st = stage ? stage + (bi * d + c) * LGCN_EMU_BLOCK : nullptr;
+                const float a = emu_slow_block<XD>(edges, bk.beg, bk.end, x, xdiv, x_nz, st, c,
+                                                   __uint_as_float(ab), sq);
+                ab = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(a));
+#ifdef LGCN_EMU_STATS
+                ++n_slow;
+                t_slow += __builtin_amdgcn_s_memtime() - t0;
+#endif
+            }
+        }
+    }
+#ifdef LGCN_EMU_STATS
+    if (lane == 0 && blockIdx.x < 256) {
+        atomicAdd(&g_emu_row_stats[blockIdx.x][0], n_fast);
+        atomicAdd(&g_emu_row_stats[blockIdx.x][1], n_slow);
+        atomicAdd(&g_emu_row_stats[blockIdx.x][2], t_slow);
+        atomicMax(&g_emu_row_stats[blockIdx.x][3], __builtin_amdgcn_s_memtime() - t_start);
+    }
+#endif
+    if (lane != 0) return;
+    const int32_t row = er.row;
+    float out = __uint_as_float(ab);
+    if constexpr (MODE == LGCN_EPI_MEAN) {
+        // ((E0 + E1) + ... + E_{K-1}) + E_K, then / (K+1)  (lightgcn.py:54)
+        float s = seg_row_x(ep.prev0, row)[c];
+        for (int i = 0; i + 1 < ep.n_prev; ++i) s = s + ep.prev_dense[i][(int64_t)row * ep.ld_prev + c];
+        s = s + out;
+        out = ep.pad ? s * __int_as_float(ep.pad) : s / ep.div;
+    } else if constexpr (MODE == LGCN_EPI_ADD) {
+        if (!ep.addend_nz || row_live_x(ep.addend_nz, row)) {
+            const float z = seg_row_x(ep.addend, row)[c];
+            out = (ep.pad ? z * __int_as_float(ep.pad) : z / ep.div) + out;
+        }
+    }
+    y[(int64_t)row * ldy + c] = out;
+}
+
+inline int herr_x(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+bool is_pow2(float x) {
+    int e;
+    return x > 0.f && frexpf(x, &e) == 0.5f;
+}
+
+template <int XD>
+int launch_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                  const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, int32_t* rel,
+                  EmuMeta* meta, float* stage, hipStream_t s) {
+    const dim3 grid((uint32_t)n_blocks, (uint32_t)((d + 63) / 64));
+    hipLaunchKernelGGL((k_emu_blocks<XD>), grid, dim3(64), 0, s, edges, blocks, x, xdiv, x_nz, d,
+                       rel, meta, stage);
+    return herr_x(hipGetLastError());
+}
+
+template <int MODE, int XD>
+int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                const lgcn_emu_row_t* rows, int32_t n_rows, const int32_t* rel, const EmuMeta* meta,
+                const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
+                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+    const dim3 grid((uint32_t)n_rows, (uint32_t)d);
+    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), 0, s, edges, blocks, rows, rel, meta,
+                       stage, x, xdiv, x_nz, d, y, ldy, ep);
+    return herr_x(hipGetLastError());
+}
+
+int xd_of(float xdiv, const uint32_t* x_nz) {
+    return (xdiv == 1.f ? 0 : is_pow2(xdiv) ? 2 : 1) | (x_nz ? 4 : 0);
+}
+
+template <int MODE>
+int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+              const lgcn_emu_row_t* rows, int32_t n_rows, const int32_t* rel, const EmuMeta* meta,
+              const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
+              int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+#define LGCN_W(XD_) \
+    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, rel, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, s);
+    switch (xd) {
+        LGCN_W(0) LGCN_W(1) LGCN_W(2) LGCN_W(4) LGCN_W(5) LGCN_W(6)
+        default: return LGCN_EINVAL;
+    }
+#undef LGCN_W
+}
+
+}  // namespace
+
+extern "C" {
+
+#ifdef LGCN_EMU_STATS
+// diagnostics builds only (not in lgcn.h): read and reset the walker counters
+int lgcn_emu_stats(unsigned long long* out_host) {
+    if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_emu_stats), sizeof(g_emu_stats)) != hipSuccess)
+        return -1;
+    unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+
+int lgcn_emu_row_stats(unsigned long long* out_host) {  // [256][4], then reset
+    if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_emu_row_stats), sizeof(g_emu_row_stats)) !=
+        hipSuccess)
+        return -1;
+    static unsigned long long z[256][4];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_row_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                    lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
+                    void* meta, float* stage, void* stream) {
+    if (n_blocks < 0 || d < 1 || d > 2048 || !(x_div > 0.f)) return LGCN_EINVAL;
+    if (n_blocks == 0) return 0;
+    if (!edges || !blocks || !rel || !meta || !x.p0) return LGCN_EINVAL;
+    const int xd = xd_of(x_div, x_nz);
+    const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    EmuMeta* mp = static_cast<EmuMeta*>(meta);
+    int32_t* rp = reinterpret_cast<int32_t*>(rel);
+#define LGCN_B(XD_) \
+    case XD_: return launch_blocks<XD_>(edges, blocks, n_blocks, x, xa, x_nz, d, rp, mp, stage, s);
+    switch (xd) {
+        LGCN_B(0) LGCN_B(1) LGCN_B(2) LGCN_B(4) LGCN_B(5) LGCN_B(6)
+        default: return LGCN_EINVAL;
+    }
+#undef LGCN_B
+}
+
+int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                  const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
+                  const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
+                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* stream) {
+    if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host) return LGCN_EINVAL;
+    if (n_rows == 0) return 0;
+    if (!edges || !blocks || !rows || !rel || !meta || !y || ldy < d || !x.p0) return LGCN_EINVAL;
+    lgcn_epilogue_t ep = *epi_host;
+    if (ep.mode == LGCN_EPI_MEAN && (ep.n_prev < 1 || ep.n_prev - 1 > LGCN_MAX_LAYERS))
+        return LGCN_EINVAL;
+    if (ep.mode == LGCN_EPI_ADD && !ep.addend.p0) return LGCN_EINVAL;
+    if (ep.mode != LGCN_EPI_STORE && !(ep.div > 0.f)) return LGCN_EINVAL;
+    // a power-of-two divisor becomes a multiply by its exact reciprocal (same rounding)
+    if (ep.mode != LGCN_EPI_STORE && is_pow2(ep.div)) {
+        const float inv = 1.0f / ep.div;
+        memcpy(&ep.pad, &inv, sizeof(inv));
+    } else {
+        ep.pad = 0;
+    }
+    const int xd = xd_of(x_div, x_nz);
+    const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const EmuMeta* mp = static_cast<const EmuMeta*>(meta);
+    const int32_t* rl = reinterpret_cast<const int32_t*>(rel);
+    switch (ep.mode) {
+        case LGCN_EPI_STORE:
+            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, s);
+        case LGCN_EPI_MEAN:
+            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, s);
+        case LGCN_EPI_ADD:
+            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, s);
+        default:
+            return LGCN_EINVAL;
+    }
+}
+
+}  // extern "C"

@@ -496,6 +496,10 @@ __global__ __launch_bounds__(kBlock) void k_layer(
         for (int q = 0; q < NV; ++q) acc[q] = T::zero();
         constexpr int UH = NV >= 8 ? 1 : 8 / NV;  // hub chunks are long: deep unroll
         accumulate<V, G, NV, UH, XD>(edges, w.beg, w.end, x, lane, dW, acc, xdiv, x_nz);
+        if (w.slot < 0) {  // a whole long row: one exact chain, epilogue in place
+            epilogue_store<V, G, NV, MODE>(ep, w.row, lane, dW, acc, y, ldy);
+            return;
+        }
         float* pr = partials + (int64_t)w.slot * d;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {

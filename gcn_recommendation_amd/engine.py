@@ -24,11 +24,40 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
-ABI_VERSION = 4
+ABI_VERSION = 5
+LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 32, 16, 256
 
-# Rows up to this degree run as one sequential fmaf chain (bitwise = reference CPU path);
-# longer rows are split into HUB_CHUNK-edge chunks. LGCN_HUB_THRESHOLD=exact disables splitting.
+# Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
+# bitwise = reference CPU path). Longer rows ("hubs") follow the hub mode:
+#   exact (default): rows up to EMU_MIN_DEGREE are whole-row chains of their own, longer rows are
+#                    reproduced exactly by block emulation (lgcn_exact.hip) — bitwise everywhere;
+#   chunk:           rows are cut into HUB_CHUNK-edge chunks summed in a fixed order (fast,
+#                    deterministic, NOT bitwise to the reference on long rows).
+# LGCN_HUB_THRESHOLD=exact puts every row in the bundles (the plain sequential chain; slow on
+# power-law hubs, kept as the unoptimised reference mode).
 DEFAULT_HUB_THRESHOLD = 128
+HUB_MODES = ("exact", "chunk")
+# Whole-row chains above this degree are emulated (LGCN_EMU_MIN_DEGREE): a chain is one lane
+# group's dependent gathers (~0.27 us per 8 edges), so 4096 edges is ~0.14 ms.
+DEFAULT_EMU_MIN_DEGREE = 4096
+
+
+def hub_mode_from_env():
+    m = os.environ.get("LGCN_HUB_MODE", "exact").lower()
+    if m not in HUB_MODES:
+        raise LgcnError(f"LGCN_HUB_MODE={m!r} ({' | '.join(HUB_MODES)})")
+    return m
+
+
+def emu_stage_enabled():
+    """LGCN_EMU_STAGE=0 turns off the staged X elements of emulated blocks (re-run blocks then
+    gather X: one 4-B element per row, a whole memory line each)."""
+    return os.environ.get("LGCN_EMU_STAGE", "1") != "0"
+
+
+def emu_min_degree_from_env():
+    v = os.environ.get("LGCN_EMU_MIN_DEGREE", "")
+    return int(v) if v else DEFAULT_EMU_MIN_DEGREE
 # Edges per hub chunk: LGCN_HUB_CHUNK, else by graph size (hub_chunk_for). A chunk is one lane
 # group's sequential chain, so it must stay short against the whole layer: on the C2 graph
 # (1.6M nonzeros, 0.07-0.1 ms per layer) 128-edge chunks run the forward 0.318 -> 0.224 ms,
@@ -54,6 +83,17 @@ class EpilogueT(ctypes.Structure):
                 ("pad", ctypes.c_int32), ("prev0", RowsT),
                 ("prev_dense", ctypes.c_void_p * LGCN_MAX_LAYERS), ("ld_prev", ctypes.c_int64),
                 ("addend", RowsT), ("addend_nz", ctypes.c_void_p)]
+
+
+class PlanT(ctypes.Structure):
+    """lgcn_hub_plan_t"""
+    _fields_ = [("items", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("partials", ctypes.c_void_p),
+                ("emu_blocks", ctypes.c_void_p), ("emu_rows", ctypes.c_void_p),
+                ("emu_rel", ctypes.c_void_p), ("emu_meta", ctypes.c_void_p),
+                ("emu_stage", ctypes.c_void_p),
+                ("threshold", ctypes.c_int32), ("n_items", ctypes.c_int32),
+                ("n_rows", ctypes.c_int32), ("n_pre", ctypes.c_int32),
+                ("n_emu_blocks", ctypes.c_int32), ("n_emu_rows", ctypes.c_int32)]
 
 
 class LgcnError(RuntimeError):
@@ -95,10 +135,16 @@ ABI = [
     ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _I32,
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
-    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _I32, _P,
-                                              RowsT, _I32, _I32, _P, _P, _P, _P]),
-    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, _I32, _I32, _P,
-                                               RowsT, _P, _I32, _I32, _P, _P, _P]),
+    ("lgcn_emu_blocks", ctypes.c_int, [_P, _P, _I32, RowsT, ctypes.c_float, _P, _I32, _P, _P, _P,
+                                       _P]),
+    ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
+                                     _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_layer", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, ctypes.c_float, _P,
+                                  _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _I32,
+                                              _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _P,
+                                               _I32, _I32, _P, _P, _P]),
 ]
 
 
@@ -217,32 +263,114 @@ def hub_threshold_from_env(default=DEFAULT_HUB_THRESHOLD):
 # graph plan: CSR + hub chunks, built once per adjacency tensor and cached on it
 # ----------------------------------------------------------------------------------------------
 class HubPlan:
-    def __init__(self, threshold, chunk, items, rows, n_slots, n_hub_rows=0, n_pre=0):
+    """How one operator's rows above the bundle threshold are summed (lgcn_hub_plan_t).
+
+    chunk mode: `items` are chunks (slot >= 0) and `rows` the combine entries (n_pre
+    pre-reductions first). exact mode: `items` are whole long rows (slot = -1: one exact chain,
+    epilogue in place) and rows above emu_min are emulated (`emu_blocks` / `emu_rows`)."""
+
+    def __init__(self, threshold, mode="exact", chunk=None, items=None, rows=None, n_slots=0,
+                 n_hub_rows=0, n_pre=0, emu_blocks=None, emu_rows=None, emu_min=None):
         self.threshold = threshold
+        self.mode = mode
         self.chunk = chunk
+        self.emu_min = emu_min
         self.items = items      # int32 [n_items, 4] device (lgcn_hub_item_t)
         self.rows = rows        # int32 [n_pre + n_rows, 4] device (lgcn_hub_row_t)
         self.n_items = 0 if items is None else items.shape[0]
-        self.n_rows = n_hub_rows  # hub rows (final entries, after the n_pre pre-reductions)
+        self.n_rows = n_hub_rows  # chunked hub rows (final entries, after the n_pre pre-reductions)
         self.n_pre = n_pre
         self.n_entries = n_pre + n_hub_rows
         self.n_slots = n_slots  # partial rows: chunk slots + pre-reduction slots
+        self.emu_blocks = emu_blocks  # int32 [n_emu_blocks, 4] (lgcn_emu_block_t)
+        self.emu_rows = emu_rows      # int32 [n_emu_rows, 4] (lgcn_emu_row_t)
+        self.n_emu_blocks = 0 if emu_blocks is None else emu_blocks.shape[0]
+        self.n_emu_rows = 0 if emu_rows is None else emu_rows.shape[0]
+        self._scratch = {}
+
+    @property
+    def n_long(self):
+        return self.n_items if self.mode == "exact" else 0
+
+    def scratch(self, d, device):
+        """(partials, emu_rel, emu_meta, emu_stage) for width d, allocated once per width and
+        reused (the layers of one operator run in stream order)."""
+        if d not in self._scratch:
+            f32 = dict(dtype=torch.float32, device=device)
+            part = torch.empty(self.n_slots * d, **f32) if self.n_slots else None
+            rel = meta = stage = None
+            if self.n_emu_blocks:
+                rel = torch.empty(self.n_emu_blocks * d * LGCN_EMU_CANDS, **f32)
+                meta = torch.empty(self.n_emu_blocks * d * LGCN_EMU_META_BYTES, dtype=torch.uint8,
+                                   device=device)
+                if emu_stage_enabled():
+                    stage = torch.empty(self.n_emu_blocks * d * LGCN_EMU_BLOCK, **f32)
+            self._scratch[d] = (part, rel, meta, stage)
+        return self._scratch[d]
+
+    def struct(self, d, device):
+        part, rel, meta, stage = self.scratch(d, device)
+        p = PlanT()
+        p.items, p.n_items = (self.items.data_ptr() if self.n_items else None), self.n_items
+        p.rows, p.n_rows, p.n_pre = (self.rows.data_ptr() if self.n_entries else None), \
+            self.n_entries, self.n_pre
+        p.partials = part.data_ptr() if part is not None else None
+        p.emu_blocks = self.emu_blocks.data_ptr() if self.n_emu_blocks else None
+        p.emu_rows = self.emu_rows.data_ptr() if self.n_emu_rows else None
+        p.n_emu_blocks, p.n_emu_rows = self.n_emu_blocks, self.n_emu_rows
+        p.emu_rel = rel.data_ptr() if rel is not None else None
+        p.emu_meta = meta.data_ptr() if meta is not None else None
+        p.emu_stage = stage.data_ptr() if stage is not None else None
+        p.threshold = min(self.threshold, INT32_MAX)
+        return p
 
 
-def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_group=None):
-    """Cut rows with degree > threshold into `chunk`-edge pieces (host planner, numpy).
-    rowptr_host is in storage (slot) order; row_ids_host maps a slot to its output row.
+def plan_emulation(rowptr_host, slots, device, row_ids_host=None):
+    """Blocks of LGCN_EMU_BLOCK edges for the emulated rows (slots, largest first)."""
+    if slots.size == 0:
+        return None, None
+    beg0 = rowptr_host[slots].astype(np.int64)
+    deg = rowptr_host[slots + 1].astype(np.int64) - beg0
+    nb = (deg + LGCN_EMU_BLOCK - 1) // LGCN_EMU_BLOCK
+    first = np.concatenate([[0], np.cumsum(nb)[:-1]])
+    ix = np.repeat(np.arange(slots.size), nb)
+    k = np.arange(int(nb.sum())) - np.repeat(first, nb)
+    beg = np.repeat(beg0, nb) + k * LGCN_EMU_BLOCK
+    end = np.minimum(beg + LGCN_EMU_BLOCK, np.repeat(beg0 + deg, nb))
+    blocks = np.stack([ix, beg, end, (k == 0).astype(np.int64)], 1).astype(np.int32)
+    out_row = slots if row_ids_host is None else row_ids_host[slots]
+    rows = np.stack([out_row, first, nb, np.zeros_like(nb)], 1).astype(np.int32)
+    return torch.from_numpy(blocks).to(device), torch.from_numpy(rows).to(device)
 
-    A hub row with more than pre_group chunks is combined in two levels: pre-reduction entries
-    (leading the row list) sum runs of pre_group consecutive chunk partials into extra partial
-    slots, and the row's final entry sums those. Without it the combine of a 2.77M-edge row
-    (10.8k partials) is one block's 85-step latency chain, longer than all other rows together."""
+
+def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_group=None,
+              mode="exact", emu_min=None):
+    """Plan the rows with degree > threshold (host planner, numpy). rowptr_host is in storage
+    (slot) order; row_ids_host maps a slot to its output row.
+
+    exact: rows up to emu_min become whole-row items (one exact chain each), longer rows are
+    emulated in blocks (plan_emulation). chunk: rows are cut into `chunk`-edge pieces; a hub row
+    with more than pre_group chunks is combined in two levels: pre-reduction entries (leading the
+    row list) sum runs of pre_group consecutive chunk partials into extra partial slots, and the
+    row's final entry sums those. Without it the combine of a 2.77M-edge row (10.8k partials) is
+    one block's 85-step latency chain, longer than all other rows together."""
     if pre_group is None:
         pre_group = DEFAULT_HUB_PRE_GROUP
+    if emu_min is None:
+        emu_min = emu_min_degree_from_env()
     deg = np.diff(rowptr_host.astype(np.int64))
     hub = np.nonzero(deg > threshold)[0]
     if threshold >= INT32_MAX or hub.size == 0:
-        return HubPlan(threshold, chunk, None, None, 0)
+        return HubPlan(threshold, mode, chunk, emu_min=emu_min)
+    out_row = hub if row_ids_host is None else row_ids_host[hub]
+    if mode == "exact":
+        long_ = deg[hub] <= emu_min
+        items = np.stack([out_row[long_], rowptr_host[hub[long_]], rowptr_host[hub[long_] + 1],
+                          np.full(int(long_.sum()), -1)], 1).astype(np.int32)
+        eb, er = plan_emulation(rowptr_host, hub[~long_], device, row_ids_host)
+        return HubPlan(threshold, mode, None,
+                       torch.from_numpy(items).to(device) if items.shape[0] else None,
+                       emu_blocks=eb, emu_rows=er, emu_min=emu_min)
     nch = (deg[hub] + chunk - 1) // chunk
     first = np.concatenate([[0], np.cumsum(nch)[:-1]])
     n_chunks = int(nch.sum())
@@ -251,7 +379,6 @@ def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_grou
     beg = rowptr_host[row_of].astype(np.int64) + k * chunk
     end = np.minimum(beg + chunk, rowptr_host[row_of + 1])
     # longest rows first so their combine inputs are ready early; items in slot order
-    out_row = hub if row_ids_host is None else row_ids_host[hub]
     items = np.stack([np.repeat(out_row, nch), beg, end, np.arange(n_chunks)], 1).astype(np.int32)
     rows = np.stack([out_row, first, nch, np.zeros_like(hub)], 1).astype(np.int64)
     pre = np.zeros((0, 4), np.int64)
@@ -268,7 +395,7 @@ def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_grou
         rows[big, 2] = ng
     n_slots = n_chunks + pre.shape[0]
     table = np.concatenate([pre, rows]).astype(np.int32)
-    return HubPlan(threshold, chunk, torch.from_numpy(items).to(device),
+    return HubPlan(threshold, mode, chunk, torch.from_numpy(items).to(device),
                    torch.from_numpy(table).to(device), n_slots, hub.size, pre.shape[0])
 
 
@@ -301,12 +428,18 @@ class Graph:
             self._row_ids_host = self.row_ids.cpu().numpy()
         return self._row_ids_host
 
-    def hubs(self, threshold, chunk=None):
+    def hubs(self, threshold, chunk=None, mode=None, emu_min=None):
+        """The hub plan for `threshold` (cached): mode / emu_min default to LGCN_HUB_MODE /
+        LGCN_EMU_MIN_DEGREE."""
+        mode = mode or hub_mode_from_env()
+        if mode not in HUB_MODES:
+            raise LgcnError(f"unknown hub mode {mode!r}")
+        emu_min = emu_min_degree_from_env() if emu_min is None else emu_min
         chunk = chunk or hub_chunk_for(self.nnz)
-        key = (threshold, chunk, DEFAULT_HUB_PRE_GROUP)
+        key = (threshold, mode) + ((chunk, DEFAULT_HUB_PRE_GROUP) if mode == "chunk" else (emu_min,))
         if key not in self._plans:
             self._plans[key] = plan_hubs(self.rowptr_host(), threshold, chunk, self.device,
-                                         self.row_ids_host())
+                                         self.row_ids_host(), mode=mode, emu_min=emu_min)
         return self._plans[key]
 
     def degrees(self):
@@ -522,28 +655,22 @@ def _check_emb(segments, d, device):
 
 def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0,
                x_nz=None):
-    """One layer Y = epilogue(Â·(X / x_div)) through lgcn_spmm_layer + lgcn_hub_combine.
+    """One layer Y = epilogue(Â·(X / x_div)) under the operator's hub plan (lgcn_layer: the
+    emulation block pass, the layer kernel, the chunk combine and the emulation walk).
     x_nz: optional row bitmask of X (rows_nonzero; ADD epilogue only)."""
     lib = load_library()
     hp = hubs or graph.hubs(hub_threshold)
-    partials = None
-    if hp.n_items:
-        partials = torch.empty(hp.n_slots * d, dtype=torch.float32, device=graph.device)
     stream = stream or _stream(graph.device)
+    plan = hp.struct(d, graph.device)
     x = rows_desc(x_segments, d)
-    _check(lib.lgcn_spmm_layer(_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids),
-                               graph.n_rows,
-                               min(hp.threshold, INT32_MAX), _ptr(hp.items), hp.n_items,
-                               _ptr(partials), x, x_div, _ptr(x_nz), _ptr(y), y.stride(0), d,
-                               ctypes.byref(epi), stream), "lgcn_spmm_layer")
-    if hp.n_rows:
-        _check(lib.lgcn_hub_combine(_ptr(hp.rows), hp.n_entries, hp.n_pre, _ptr(partials), _ptr(y),
-                                    y.stride(0), d, ctypes.byref(epi), stream), "lgcn_hub_combine")
+    _check(lib.lgcn_layer(_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids),
+                          graph.n_rows, ctypes.byref(plan), x, x_div, _ptr(x_nz), _ptr(y),
+                          y.stride(0), d, ctypes.byref(epi), stream), "lgcn_layer")
     return y
 
 
 def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
-                      return_layers=False):
+                      return_layers=False, hub_mode=None, emu_min=None):
     """final = mean(E0, Â E0, ..., Â^K E0) with E0 = cat(segments) (never materialised).
 
     layer_events: optional list of (start, end) torch.cuda.Event pairs recorded around each
@@ -567,7 +694,7 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
         if K == 0:
             _check(lib.lgcn_scale_rows(e0, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
             return (out, []) if return_layers else out
-        hp = graph.hubs(hub_threshold)
+        hp = graph.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         layers = [torch.empty((n, d), dtype=torch.float32, device=dev) for _ in range(K - 1)]
         for k in range(1, K + 1):
             xs = segments if k == 1 else [layers[k - 2]]
@@ -626,7 +753,8 @@ def _sparse_grad_mode():
     return m
 
 
-def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None):
+def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_mode=None,
+                       emu_min=None):
     """dE0 = Σ_k (Âᵀ)^k G/(K+1), Horner order h = G/(K+1) + Âᵀ h (autograd's accumulation).
 
     grad_out: the [n x d] upstream gradient, or a list of row blocks (the user / item / brand
@@ -651,7 +779,7 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None):
         if K == 0:
             _check(lib.lgcn_scale_rows(g, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
             return out
-        hp = gt.hubs(hub_threshold)
+        hp = gt.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         mode = sparse or _sparse_grad_mode()
         nz = None
         if mode == "on" or (mode == "auto" and n > 0 and

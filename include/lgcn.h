@@ -26,10 +26,12 @@
  *    it is non-NULL the CSR rows are stored in slots (lgcn_csr_order_by_degree): slot s holds
  *    the edges of row row_ids[s] and its result is written to row row_ids[s]. Column ids, X, Y
  *    and the epilogue operands are always in row-id space; only the work order changes.
- *  - Numerics: rows of degree <= hub_threshold are summed by one sequential fmaf chain in stored
- *    order, the exact arithmetic of ATen's addmm_sparse_dense_cpu loop that torch.sparse.mm runs
- *    on CPU (bitwise identical results). Rows above the threshold ("hubs") are cut into fixed
- *    chunks summed in a fixed order (deterministic, not bitwise to the CPU order).
+ *  - Numerics: every row is the exact arithmetic of ATen's addmm_sparse_dense_cpu loop that
+ *    torch.sparse.mm runs on CPU — one sequential fmaf chain per row in stored order — so
+ *    results are bitwise identical, under an exact hub plan (lgcn_hub_plan_t without chunk
+ *    items): short rows run that chain directly, rows of any length up to millions of edges are
+ *    reproduced by block emulation (lgcn_emu_*). Hub CHUNK items are the optional fast mode: a
+ *    long row cut into fixed chunks summed in a fixed order (deterministic, not bitwise).
  */
 #ifndef LGCN_H_
 #define LGCN_H_
@@ -41,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 4
+#define LGCN_ABI_VERSION 5
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -75,7 +77,9 @@ typedef struct {
 } lgcn_rows_t;
 
 /* hub work: one chunk of one long row -> one partial-sum slot of d floats (beg/end index the
- * edge array as stored, i.e. in slot order when the CSR is degree-ordered) */
+ * edge array as stored, i.e. in slot order when the CSR is degree-ordered). slot < 0: the item
+ * is a WHOLE row, summed as one sequential chain (bitwise = reference) with the epilogue applied
+ * in place to output row `row` (exact plans: rows between the bundle and emulation sizes). */
 typedef struct {
     int32_t row;
     int32_t beg;
@@ -93,6 +97,56 @@ typedef struct {
     int32_t n_slots;
     int32_t pad;
 } lgcn_hub_row_t;
+
+/* ---- exact hub rows: parallel reproduction of one long sequential chain (lgcn_exact.hip) ---- */
+#define LGCN_EMU_BLOCK 256       /* max edges per emulation block */
+#define LGCN_EMU_CANDS 32        /* candidate chains per (block, column): 16 binades x 2 signs */
+#define LGCN_EMU_META_BYTES 16   /* per (block, column) metadata record (opaque) */
+
+/* one block of an emulated row: edges [beg, end) as stored; first = 1 for the row's block 0;
+ * row = index of its lgcn_emu_row_t (informational) */
+typedef struct {
+    int32_t row;
+    int32_t beg;
+    int32_t end;
+    int32_t first;
+} lgcn_emu_block_t;
+
+/* one emulated row: output row id, its blocks [first_block, first_block + n_blocks) in edge
+ * order in the block list */
+typedef struct {
+    int32_t row;
+    int32_t first_block;
+    int32_t n_blocks;
+    int32_t pad;
+} lgcn_emu_row_t;
+
+/* Everything a layer needs beyond the CSR to treat rows above the bundle threshold:
+ *  - items/n_items: hub chunks (slot >= 0, combined by `rows`) and whole long rows (slot < 0);
+ *  - rows/n_rows/n_pre/partials: the chunk combine (lgcn_hub_combine); n_rows = 0 if none;
+ *  - emu_*: rows reproduced exactly by block emulation (lgcn_emu_blocks + lgcn_emu_walk);
+ *    emu_rel [n_emu_blocks x d x LGCN_EMU_CANDS] 4-byte words and emu_meta [n_emu_blocks x d x
+ *    LGCN_EMU_META_BYTES] are caller scratch; emu_stage (optional, NULL = off) [n_emu_blocks x
+ *    d x LGCN_EMU_BLOCK] fp32 scratch: the block pass writes each block's X elements per column
+ *    there, so a block the walk must re-run reads them contiguously instead of gathering.
+ * threshold: rows of degree <= threshold run as bundles in the layer kernel; every row above it
+ * must be covered by exactly one of: chunk items, a long-row item, an emulated row. */
+typedef struct {
+    const lgcn_hub_item_t* items;
+    const lgcn_hub_row_t* rows;
+    float* partials;
+    const lgcn_emu_block_t* emu_blocks;
+    const lgcn_emu_row_t* emu_rows;
+    float* emu_rel;
+    void* emu_meta;
+    float* emu_stage;
+    int32_t threshold;
+    int32_t n_items;
+    int32_t n_rows;
+    int32_t n_pre;
+    int32_t n_emu_blocks;
+    int32_t n_emu_rows;
+} lgcn_hub_plan_t;
 
 /* Epilogue operands. MEAN: prev0 is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
  * dense layer buffers E1..E_{n_prev-1} with leading dimension ld_prev, div = K+1. ADD: addend
@@ -235,30 +289,46 @@ int lgcn_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t d, uint32_t* mask, 
 int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
                     void* stream);
 
+/* Emulation block pass for one layer: for every block of every emulated row, candidate chains
+ * + bounds over X (read as lgcn_spmm_layer reads it: x_div, x_nz) into rel / meta, and (stage
+ * != NULL) the block's X elements per column into stage. */
+int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                    lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
+                    void* meta, float* stage, void* stream);
+
+/* Emulation walk: each emulated row's final value per column (bitwise the sequential chain),
+ * epilogue applied, written to Y. Needs lgcn_emu_blocks' rel / meta (and stage, if it wrote
+ * one; NULL = re-run blocks gather X) of the same X. */
+int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                  const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
+                  const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
+                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* stream);
+
+/* One whole layer under a hub plan: emulation block pass, lgcn_spmm_layer (bundles, chunks and
+ * long rows), chunk combine, emulation walk — every row of Y written once. */
+int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+               int32_t n_rows, const lgcn_hub_plan_t* plan, lgcn_rows_t x, float x_div,
+               const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
+               const lgcn_epilogue_t* epi_host, void* stream);
+
 /* Whole forward in one call: E1..E_{K-1} into layer_bufs_host[0..K-2] (each [n x d], ld = d),
- * final = mean(E0..EK) into out [n x d]. emb = E0 segments. Hub plan as in lgcn_spmm_layer
- * (partials sized for it). ev_host: NULL or 2*K hipEvent_t recorded around each layer's
- * lgcn_spmm_layer launch (timing only). */
+ * final = mean(E0..EK) into out [n x d]. emb = E0 segments. plan: as in lgcn_layer (its
+ * scratch sized for d). ev_host: NULL or 2*K hipEvent_t recorded around each layer (timing
+ * only). */
 int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
-                           const int32_t* row_ids, int32_t n,
-                           int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
-                           int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                           int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                           const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                            lgcn_rows_t emb, int32_t d,
                            int32_t K, float* const* layer_bufs_host, float* out,
                            void* const* ev_host, void* stream);
 
 /* Whole backward: grad_e0 = sum_k (Âᵀ)^k G/(K+1) in the Horner order autograd uses
- * (c = G/(K+1); h = c; K times h = c + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric).
- * G is read in place as segments (the user/item/brand output grads); c is never stored.
- * grad_nz: NULL, or G's row bitmask (lgcn_rows_nonzero): a BPR batch touches a few thousand
- * rows, so the first layer gathers only those and no epilogue reads G's zero rows.
- * work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. */
+ * (c = G/(K+1); h = c; K times h = c + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric)
+ * and plan its hub plan. G is read in place as segments (the user/item/brand output grads); c
+ * is never stored. grad_nz: NULL, or G's row bitmask (lgcn_rows_nonzero): a BPR batch touches
+ * a few thousand rows, so the first layer gathers only those and no epilogue reads G's zero
+ * rows. work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. */
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
-                            const int32_t* row_ids, int32_t n,
-                            int32_t hub_threshold, const lgcn_hub_item_t* hub_items,
-                            int32_t n_hub_items, const lgcn_hub_row_t* hub_rows,
-                            int32_t n_hub_rows, int32_t n_pre_rows, float* partials,
+                            const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                             lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                             float* grad_e0, void* stream);

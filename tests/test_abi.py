@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 4
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 5
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -70,8 +70,20 @@ def test_argument_validation_without_gpu(lib):
     assert lib.lgcn_hub_combine(None, 4, 5, None, None, 64, 64, ctypes.byref(ep), None) == -1
     assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 64, None, None, None) == -1
     assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 0, None, None, None) == -1
-    assert lib.lgcn_propagate_forward(None, None, None, 5, 0, None, 0, None, 0, 0, None, rows, 64, -1,
+    assert lib.lgcn_propagate_forward(None, None, None, 5, None, rows, 64, -1,
                                       None, None, None, None) == -1
+    plan = engine.PlanT()
+    plan.n_emu_rows = 3  # emulated rows without their buffers
+    ep.mode = engine.LGCN_EPI_STORE
+    assert lib.lgcn_layer(None, None, None, 0, ctypes.byref(plan), rows, 1.0, None, None, 64, 64,
+                          ctypes.byref(ep), None) == -1
+    assert lib.lgcn_layer(None, None, None, 0, None, rows, 1.0, None, None, 64, 64,
+                          ctypes.byref(ep), None) == -1
+    assert lib.lgcn_emu_blocks(None, None, -1, rows, 1.0, None, 64, None, None, None, None) == -1
+    assert lib.lgcn_emu_blocks(None, None, 0, rows, 1.0, None, 64, None, None, None, None) == 0
+    assert lib.lgcn_emu_walk(None, None, None, 2, None, None, None, rows, 1.0, None, None, 64, 64,
+                             ctypes.byref(ep), None) == -1
+    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 0
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
                                   ctypes.byref(nbytes), None) == -1

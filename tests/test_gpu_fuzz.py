@@ -1,9 +1,11 @@
 """Seeded fuzz of the HIP propagation against the oracle (the reference's CPU arithmetic):
 random sizes (1..4000 rows), widths (d = 1..256, aligned and not), depths (K = 0..4), COO
 shapes (symmetric row-sorted like main.py's Â, unsorted with duplicate coordinates, skewed with
-hub rows, mostly-empty rows), both storage orders, single-row and bundled lane groups. Exact mode
-must be bitwise for the forward and the backward (dense and row-sparse upstream gradients); the
-default hub chunking must stay within the north_star tolerance."""
+hub rows, mostly-empty rows), both storage orders, single-row and bundled lane groups. The plain
+chain mode and the default exact hub plan (long rows as whole-row chains, longer rows emulated by
+blocks — thresholds lowered so these small graphs exercise both) must be bitwise for the forward
+and the backward (dense and row-sparse upstream gradients); the optional hub chunking must stay
+within the north_star tolerance."""
 import numpy as np
 import pytest
 import torch
@@ -72,10 +74,20 @@ def test_fuzz_forward_backward(gpu_device, monkeypatch, case):
         got_s = engine.propagate_backward(g, torch.from_numpy(Gs).to(gpu_device), K,
                                           engine.INT32_MAX, sparse="on").cpu().numpy()
         assert np.array_equal(got_s, oracle.backward(r, c, v, Gs, K)), (case, "sparse backward")
-        # default hub chunking (a low threshold so small graphs have hubs): deterministic and
-        # within the north_star tolerance
-        f1 = engine.propagate_forward(g, x, K, hub_threshold=8).cpu().numpy()
-        f2 = engine.propagate_forward(g, x, K, hub_threshold=8).cpu().numpy()
+        # the default exact hub plan with low thresholds: rows above 8 edges are whole-row
+        # chains, above 16 emulated — bitwise, forward and both backward paths
+        kw = dict(hub_threshold=8, hub_mode="exact", emu_min=16)
+        got = engine.propagate_forward(g, x, K, **kw).cpu().numpy()
+        assert np.array_equal(got, want), (case, "exact plan forward")
+        got_b = engine.propagate_backward(g, torch.from_numpy(G).to(gpu_device), K, sparse="off",
+                                          **kw).cpu().numpy()
+        assert np.array_equal(got_b, want_b), (case, "exact plan backward")
+        got_s = engine.propagate_backward(g, torch.from_numpy(Gs).to(gpu_device), K, sparse="on",
+                                          **kw).cpu().numpy()
+        assert np.array_equal(got_s, oracle.backward(r, c, v, Gs, K)), (case, "exact sparse bwd")
+        # optional hub chunking: deterministic and within the north_star tolerance
+        f1 = engine.propagate_forward(g, x, K, hub_threshold=8, hub_mode="chunk").cpu().numpy()
+        f2 = engine.propagate_forward(g, x, K, hub_threshold=8, hub_mode="chunk").cpu().numpy()
         assert np.array_equal(f1, f2)
         if want.size and np.abs(want).max() > 0:
             assert_close_normwise(f1, want, what=f"case {case} chunked")

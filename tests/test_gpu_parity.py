@@ -216,7 +216,11 @@ def test_row_bundles_bitwise(gpu_device, d, order):
                 lib.lgcn_tune(engine.TUNE_MEAN_PREFETCH, pf)
                 got = engine.propagate_forward(g, x, K, hub_threshold=engine.INT32_MAX)
                 assert np.array_equal(got.cpu().numpy(), want), (d, K, pf)
-                chunked.append(engine.propagate_forward(g, x, K, hub_threshold=24).cpu().numpy())
+                chunked.append(engine.propagate_forward(g, x, K, hub_threshold=24,
+                                                        hub_mode="chunk").cpu().numpy())
+                ex = engine.propagate_forward(g, x, K, hub_threshold=24, hub_mode="exact",
+                                              emu_min=48)
+                assert np.array_equal(ex.cpu().numpy(), want), (d, K, pf, "exact plan")
             assert np.array_equal(chunked[0], chunked[1]), (d, K)
             assert_close_normwise(chunked[0], want, what=f"chunked d={d} K={K}")
     finally:
@@ -225,66 +229,70 @@ def test_row_bundles_bitwise(gpu_device, d, order):
 
 
 @ORDERS
-@pytest.mark.parametrize("thr", [16, "exact"])
-def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, thr):
+@pytest.mark.parametrize("mode", ["chunk", "exact", "chain"])
+def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
     """lgcn_propagate_forward / lgcn_propagate_backward — the one-call entry points a C host
     binds — equal the per-layer path the Python binding drives, bitwise,
-    with chunked hub rows and two-level combines (pre_group 2); exact mode equals the oracle."""
+    under each hub plan: chunked hub rows with two-level combines (pre_group 2), the exact plan
+    (whole long rows + emulated rows: bitwise = oracle) and no hub plan at all (chain)."""
     import ctypes
     monkeypatch.setattr(engine, "DEFAULT_HUB_PRE_GROUP", 2)
     monkeypatch.setattr(engine, "DEFAULT_HUB_CHUNK", 8)   # hub_d32's rows reach degree 60
     z = load_case("hub_d32")
     U, I, B, d, K = case_dims(z)
     n = U + I + B
-    thr = engine.INT32_MAX if thr == "exact" else thr
+    thr = engine.INT32_MAX if mode == "chain" else 16
+    kw = dict(mode="chunk" if mode == "chunk" else "exact", emu_min=32)
     lib = engine.load_library()
     P = engine._ptr
     g = engine.graph_from_coo(_adj(z, gpu_device))
     segs = [torch.from_numpy(z[f"param/{k}_embedding.weight"]).to(gpu_device)
             for k in ("user", "item", "brand")]
     st = engine._stream(gpu_device)
-    hp = g.hubs(thr)
-    if thr == 16:
+    hp = g.hubs(thr, **kw)
+    if mode == "chunk":
         assert hp.n_pre > 0
+    if mode == "exact":
+        assert hp.n_emu_rows > 0 and hp.n_long > 0
+    plan = hp.struct(d, gpu_device)
     layers = [torch.empty((n, d), device=gpu_device) for _ in range(K - 1)]
     out = torch.empty((n, d), device=gpu_device)
-    part = torch.empty(max(hp.n_slots, 1) * d, device=gpu_device)
     bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
-    rc = lib.lgcn_propagate_forward(P(g.rowptr), P(g.edges), P(g.row_ids), n, thr, P(hp.items),
-                                    hp.n_items, P(hp.rows), hp.n_entries, hp.n_pre, P(part),
-                                    engine.rows_desc(segs, d), d, K, ctypes.cast(bufs, ctypes.c_void_p),
-                                    P(out), None, st)
+    rc = lib.lgcn_propagate_forward(P(g.rowptr), P(g.edges), P(g.row_ids), n, ctypes.byref(plan),
+                                    engine.rows_desc(segs, d), d, K,
+                                    ctypes.cast(bufs, ctypes.c_void_p), P(out), None, st)
     assert rc == 0
-    want = engine.propagate_forward(g, segs, K, thr)
+    want = engine.propagate_forward(g, segs, K, thr, hub_mode=kw["mode"], emu_min=32)
     assert torch.equal(out, want)
     ref = oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], case_e0(z), K)
-    if thr == engine.INT32_MAX:
+    if mode != "chunk":
         assert np.array_equal(out.cpu().numpy(), ref)
     else:  # chunked + two-level combined rows: the north_star tolerance
         assert_close_normwise(out.cpu().numpy(), ref, what="two-level combine")
     G = torch.from_numpy(upstream_grad(n, d)).to(gpu_device)
     gt = g.transpose
-    hpt = gt.hubs(thr)
+    plan_t = gt.hubs(thr, **kw).struct(d, gpu_device)
     work = torch.empty((n, d), device=gpu_device)
     ge0 = torch.empty((n, d), device=gpu_device)
-    part_t = torch.empty(max(hpt.n_slots, 1) * d, device=gpu_device)
-    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n, thr,
-                                     P(hpt.items), hpt.n_items, P(hpt.rows), hpt.n_entries,
-                                     hpt.n_pre, P(part_t), engine.rows_desc([G], d), None, d, K,
+    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n,
+                                     ctypes.byref(plan_t), engine.rows_desc([G], d), None, d, K,
                                      P(work), P(ge0), st)
     assert rc == 0
-    assert torch.equal(ge0, engine.propagate_backward(g, [G], K, thr, sparse="off"))
+    bkw = dict(sparse="off", hub_mode=kw["mode"], emu_min=32)
+    assert torch.equal(ge0, engine.propagate_backward(g, [G], K, thr, **bkw))
+    if mode != "chunk":
+        assert np.array_equal(ge0.cpu().numpy(), oracle.backward(
+            z["adj_row"], z["adj_col"], z["adj_val"], upstream_grad(n, d), K))
     # row-sparse upstream gradient through the C entry point's grad_nz path
     Gs = torch.zeros_like(G)
     live = torch.arange(0, n, 97, device=gpu_device)
     Gs[live] = G[live]
     nz, _ = engine.rows_nonzero([Gs], d, gpu_device)
-    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n, thr,
-                                     P(hpt.items), hpt.n_items, P(hpt.rows), hpt.n_entries,
-                                     hpt.n_pre, P(part_t), engine.rows_desc([Gs], d), P(nz), d, K,
+    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n,
+                                     ctypes.byref(plan_t), engine.rows_desc([Gs], d), P(nz), d, K,
                                      P(work), P(ge0), st)
     assert rc == 0
-    assert torch.equal(ge0, engine.propagate_backward(g, [Gs], K, thr, sparse="off"))
+    assert torch.equal(ge0, engine.propagate_backward(g, [Gs], K, thr, **bkw))
 
 
 def test_segments_and_misaligned_rows(gpu_device):

@@ -1,4 +1,5 @@
-"""Host planner for long ("hub") rows: chunks tile each hub row exactly, in order."""
+"""Host planner for long ("hub") rows: chunks tile each hub row exactly, in order; the exact plan
+covers every hub row once (whole-row items or emulation blocks of <= 256 edges, in edge order)."""
 import numpy as np
 
 from gcn_recommendation_amd import engine
@@ -7,7 +8,7 @@ from gcn_recommendation_amd import engine
 def test_plan_covers_hub_rows_exactly():
     deg = np.array([0, 3, 700, 1, 2000, 512, 513])
     rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
-    hp = engine.plan_hubs(rowptr, 512, 256, "cpu", pre_group=0)
+    hp = engine.plan_hubs(rowptr, 512, 256, "cpu", pre_group=0, mode="chunk")
     items = hp.items.numpy()
     rows = hp.rows.numpy()
     assert hp.n_pre == 0 and hp.n_rows == hp.n_entries == 3
@@ -28,7 +29,7 @@ def test_two_level_combine_plan():
     exactly those new slots; rows with few chunks are untouched."""
     deg = np.array([5, 300, 10 ** 5 + 7, 4096, 1000])
     rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
-    hp = engine.plan_hubs(rowptr, 128, 256, "cpu", pre_group=8)
+    hp = engine.plan_hubs(rowptr, 128, 256, "cpu", pre_group=8, mode="chunk")
     items, tab = hp.items.numpy(), hp.rows.numpy()
     n_chunks = items.shape[0]
     assert n_chunks == 2 + 391 + 16 + 4
@@ -55,8 +56,33 @@ def test_two_level_combine_plan():
 
 def test_two_level_plan_without_big_rows():
     rowptr = np.array([0, 300, 301, 900], dtype=np.int32)
-    hp = engine.plan_hubs(rowptr, 128, 256, "cpu", pre_group=8)
+    hp = engine.plan_hubs(rowptr, 128, 256, "cpu", pre_group=8, mode="chunk")
     assert hp.n_pre == 0 and hp.n_rows == 2 and hp.n_slots == 2 + 3
+
+
+def test_exact_plan_covers_every_hub_row_once():
+    deg = np.array([0, 3, 700, 1, 2000, 512, 513, 256 * 70 + 1, 129, 128])
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    row_ids = np.arange(deg.size)[::-1].astype(np.int32)  # slot s holds row n-1-s
+    hp = engine.plan_hubs(rowptr, 128, None, "cpu", row_ids_host=row_ids, mode="exact",
+                          emu_min=600)
+    items = hp.items.numpy()
+    assert (items[:, 3] == -1).all() and hp.n_rows == 0 and hp.n_slots == 0
+    long_slots = [s for s in range(deg.size) if 128 < deg[s] <= 600]
+    assert list(items[:, 0]) == [row_ids[s] for s in long_slots]
+    assert list(items[:, 1]) == [rowptr[s] for s in long_slots]
+    assert list(items[:, 2]) == [rowptr[s + 1] for s in long_slots]
+    blocks, rows = hp.emu_blocks.numpy(), hp.emu_rows.numpy()
+    emu_slots = [s for s in range(deg.size) if deg[s] > 600]
+    assert list(rows[:, 0]) == [row_ids[s] for s in emu_slots]
+    for k, s in enumerate(emu_slots):
+        _, first, nb, _ = rows[k]
+        b = blocks[first:first + nb]
+        assert (b[:, 0] == k).all() and b[0, 3] == 1 and (b[1:, 3] == 0).all()
+        assert b[0, 1] == rowptr[s] and b[-1, 2] == rowptr[s + 1]
+        assert (b[1:, 1] == b[:-1, 2]).all() and ((b[:, 2] - b[:, 1]) <= 256).all()
+        assert nb == -(-deg[s] // 256)
+    assert hp.n_emu_blocks == sum(-(-deg[s] // 256) for s in emu_slots)
 
 
 def test_exact_mode_has_no_hubs():

@@ -1,0 +1,119 @@
+"""Probe of the exact hub path on the C3 power-law graph: plan sizes, per-layer times, and (with
+a LGCN_EMU_STATS build loaded through LGCN_LIB) the walker's fast/slow block decisions.
+
+    python tools/exact_probe.py [--emu-min N] [--config c3] [--reps 3]
+    python -m gcn_recommendation_amd._build emustats LGCN_EMU_STATS=1  # then LGCN_LIB=... --stats
+"""
+import argparse
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from gcn_recommendation_amd import engine  # noqa: E402
+
+NAMES = ["fast", "slow", "identity", "slow:zero/subn", "slow:window", "slow:tie", "slow:bounds",
+         "slow steps"]
+
+
+def stats(lib):
+    buf = (ctypes.c_ulonglong * 8)()
+    assert lib.lgcn_emu_stats(buf) == 0
+    return dict(zip(NAMES, list(buf)))
+
+
+def row_stats(lib, hp, d):
+    buf = (ctypes.c_ulonglong * 1024)()
+    assert lib.lgcn_emu_row_stats(buf) == 0
+    a = np.array(buf, dtype=np.float64).reshape(256, 4)
+    rows = hp.emu_rows.cpu().numpy()
+    for k in list(range(min(8, len(rows)))) + [min(len(rows), 256) - 1]:
+        f, s_, ts, tmax = a[k]
+        nb = rows[k, 2]
+        print(f"  row {k}: {nb} blocks x {d} cols: fast {f / d:.0f} slow {s_ / d:.0f} per col "
+              f"({100 * s_ / max(f + s_, 1):.1f}%), slow cycles/slow block "
+              f"{ts / max(s_, 1):.0f}, max wave time {tmax / 2.1e3:.0f} us (at 2.1 GHz)",
+              flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--gen", default="powerlaw")
+    ap.add_argument("--emu-min", type=int, default=None)
+    ap.add_argument("--thr", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--walk", action="store_true", help="time layer 1's walk on row subsets")
+    a = ap.parse_args()
+    cfg = bench.CONFIGS[a.config]
+    dev = torch.device("cuda:0")
+    lib = engine.load_library()
+    if a.stats:
+        lib.lgcn_emu_stats.argtypes = [ctypes.c_void_p]
+        lib.lgcn_emu_row_stats.argtypes = [ctypes.c_void_p]
+    r, c, v, _, _, _ = bench.make_graph(cfg, a.gen, 16)
+    U, I, B = cfg["users"], cfg["items"], cfg.get("brands", 0)
+    n, d, K = U + I + B, cfg["d"], cfg["K"]
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack((r, c))), torch.from_numpy(v),
+                                  (n, n)).to(dev)
+    g = engine.graph_from_coo(adj)
+    gen = torch.Generator().manual_seed(42)
+    segs = [bench.xavier(U, d, gen).to(dev), bench.xavier(I, d, gen).to(dev)]
+    hp = g.hubs(a.thr, mode="exact", emu_min=a.emu_min)
+    deg = np.sort(g.degrees())[::-1]
+    print(f"plan: long rows {hp.n_long}, emulated rows {hp.n_emu_rows} ({hp.n_emu_blocks} blocks, "
+          f"{int(deg[:hp.n_emu_rows].sum()):,} edges), emu_min {hp.emu_min}; top degrees "
+          f"{deg[:6].tolist()}", flush=True)
+    for rep in range(a.reps):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(K)]
+        torch.cuda.synchronize()
+        t0 = time.time()
+        engine.propagate_forward(g, segs, K, a.thr, layer_events=ev, hub_mode="exact",
+                                 emu_min=a.emu_min)
+        torch.cuda.synchronize()
+        print(f"rep {rep}: {1e3 * (time.time() - t0):.2f} ms wall; per layer "
+              f"{[round(x.elapsed_time(y), 3) for x, y in ev]}", flush=True)
+        if a.stats:
+            print("  walker decisions (all layers):", stats(lib), flush=True)
+            row_stats(lib, hp, d)
+    if a.walk:
+        walk_timing(g, segs, d, a.thr, a.emu_min)
+
+
+
+
+def walk_timing(g, segs, d, thr, emu_min):
+    """Layer 1's emulation walk timed on subsets of the emulated rows (isolated critical path
+    vs the crowd)."""
+    import ctypes as C
+    lib = engine.load_library()
+    hp = g.hubs(thr, mode="exact", emu_min=emu_min)
+    plan = hp.struct(d, g.device)
+    x = engine.rows_desc(segs, d)
+    st = engine._stream(g.device)
+    y = torch.empty((g.n_rows, d), device=g.device)
+    ep = engine._epilogue(engine.LGCN_EPI_STORE)
+    assert lib.lgcn_emu_blocks(engine._ptr(g.edges), plan.emu_blocks, hp.n_emu_blocks, x, 1.0, None,
+                               d, plan.emu_rel, plan.emu_meta, plan.emu_stage, st) == 0
+    rows = hp.emu_rows
+    for lo, hi in ((0, 1), (1, 2), (0, 8), (8, hp.n_emu_rows), (0, hp.n_emu_rows)):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        assert lib.lgcn_emu_walk(engine._ptr(g.edges), plan.emu_blocks, rows[lo:].data_ptr(),
+                                 hi - lo, plan.emu_rel, plan.emu_meta, plan.emu_stage, x, 1.0,
+                                 None, engine._ptr(y), d, d, C.byref(ep), st) == 0
+        b.record()
+        torch.cuda.synchronize()
+        print(f"  walk rows [{lo}, {hi}): {a.elapsed_time(b):.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
