@@ -255,54 +255,82 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
 // ---------------------------------------------------------------------------------------------
 // walker: one wave per (hub row, column). The chain value is wave-uniform.
 // ---------------------------------------------------------------------------------------------
-// The block's steps as the reference runs them: a = fma(val_j, x_j, a) in stored order. All
-// (val, x) pairs are fetched at once (<= 4 per lane, one round trip) into LDS, then every lane
-// runs the same chain (the result is wave-uniform).
+// A block the walk re-runs as the reference does: a = fma(val_j, x_j, a) in stored order.
+// SlowData holds one lane's share of a block's (val, x) pairs, fetched with every load in
+// flight at once: x from the staged copy (contiguous) or gathered from X (a second round trip).
+struct SlowData {
+    int2 rec[LGCN_EMU_BLOCK / 64];   // edge records of steps t * 64 + lane
+    float xg[LGCN_EMU_BLOCK / 64];   // gathered x of the same steps (no stage)
+    float4 xs;                       // staged x of steps 4 * lane .. 4 * lane + 3
+};
+
 template <int XD>
-__device__ float emu_slow_block(const lgcn_edge_t* __restrict__ edges, int32_t beg, int32_t end,
-                                const lgcn_rows_t& x, float xdiv, const uint32_t* __restrict__ x_nz,
-                                const float* __restrict__ st, int c, float a, float2* sq) {
+__device__ __forceinline__ void slow_load(SlowData& sd, const lgcn_edge_t* __restrict__ edges,
+                                          int32_t beg, int32_t end, const lgcn_rows_t& x,
+                                          float xdiv, const uint32_t* __restrict__ x_nz,
+                                          const float* __restrict__ st, int c) {
+    constexpr int Q = LGCN_EMU_BLOCK / 64;
     const int lane = threadIdx.x;
     const int n = end - beg;
+#pragma unroll
+    for (int t = 0; t < Q; ++t)  // clamped addresses, masked values: all loads in flight
+        sd.rec[t] = *reinterpret_cast<const int2*>(edges + beg + min(t * 64 + lane, n - 1));
+    if (st) {
+        sd.xs = *reinterpret_cast<const float4*>(st + 4 * lane);
+    } else {
+#pragma unroll
+        for (int t = 0; t < Q; ++t)
+            sd.xg[t] = load_elem<XD>(x, x_nz, sd.rec[t].x, c, xdiv, t * 64 + lane < n);
+    }
+}
+
+__device__ __forceinline__ float slow_run(const SlowData& sd, int n, bool staged, float a,
+                                          float2* sq) {
     constexpr int Q = LGCN_EMU_BLOCK / 64;
-    int2 rec[Q];
+    const int lane = threadIdx.x;
+    __syncthreads();  // the previous chain's reads of sq are done
 #pragma unroll
-    for (int t = 0; t < Q; ++t)  // every record load in flight at once (clamped, masked below)
-        rec[t] = *reinterpret_cast<const int2*>(edges + beg + min(t * 64 + lane, n - 1));
-    float2 q[Q];
-    if (st) {  // the block pass staged this column's elements: contiguous, no dependent gather
-        const float4 xs = *reinterpret_cast<const float4*>(st + 4 * lane);
-        const float xv[4] = {xs.x, xs.y, xs.z, xs.w};
-        // step 4 * lane + t  ->  LDS slot; written below in (t * 64 + lane) order, so first
-        // exchange through LDS
-#pragma unroll
-        for (int t = 0; t < Q; ++t) {
-            const bool in = t * 64 + lane < n;
-            q[t] = make_float2(in ? __int_as_float(rec[t].y) : 0.f, 0.f);
-        }
+    for (int t = 0; t < Q; ++t) {
+        const bool in = t * 64 + lane < n;
+        sq[t * 64 + lane] = make_float2(in ? __int_as_float(sd.rec[t].y) : 0.f,
+                                        staged ? 0.f : sd.xg[t]);
+    }
+    if (staged) {
         __syncthreads();
-#pragma unroll
-        for (int t = 0; t < Q; ++t) sq[t * 64 + lane] = q[t];
-        __syncthreads();
+        const float xv[4] = {sd.xs.x, sd.xs.y, sd.xs.z, sd.xs.w};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             if (4 * lane + t < n) sq[4 * lane + t].y = xv[t];
-        __syncthreads();
-    } else {
-#pragma unroll
-        for (int t = 0; t < Q; ++t) {  // then every element load
-            const bool in = t * 64 + lane < n;
-            q[t] = make_float2(in ? __int_as_float(rec[t].y) : 0.f,
-                               load_elem<XD>(x, x_nz, rec[t].x, c, xdiv, in));
-        }
     }
-    if (!st) {
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < LGCN_EMU_BLOCK / 64; ++t) sq[t * 64 + lane] = q[t];
-        __syncthreads();
-    }
+    __syncthreads();
     int i = 0;
+    if (n == LGCN_EMU_BLOCK) {
+        // full block: the LDS reads run PF groups of 8 steps ahead of the FMAs, so only the
+        // dependent FMA chain is on the critical path
+        constexpr int NG = LGCN_EMU_BLOCK / 8, PF = 4;
+        float4 w[PF][4];
+#pragma unroll
+        for (int g = 0; g < PF; ++g)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[g][k] = reinterpret_cast<const float4*>(sq + 8 * g)[k];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            float4 cur[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[k] = w[g % PF][k];
+            if (g + PF < NG) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    w[g % PF][k] = reinterpret_cast<const float4*>(sq + 8 * (g + PF))[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a = __builtin_fmaf(cur[k].x, cur[k].y, a);
+                a = __builtin_fmaf(cur[k].z, cur[k].w, a);
+            }
+        }
+        return a;
+    }
     for (; i + 8 <= n; i += 8) {
         float2 w[8];
 #pragma unroll
@@ -320,45 +348,44 @@ __device__ float emu_slow_block(const lgcn_edge_t* __restrict__ edges, int32_t b
 __device__ unsigned long long g_emu_stats[8];
 // per emulated row (first 256 rows): fast blocks, slow blocks, cycles in slow blocks, max cycles
 __device__ unsigned long long g_emu_row_stats[256][4];
+#endif
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+// timing experiments only: 1 = re-run blocks skip their chain, 2 = every block translates
+__device__ int g_emu_mode;
+#define LGCN_EMU_FORCE(f) do { if (g_emu_mode == 2) (f) = true; } while (0)
+#else
+#define LGCN_EMU_FORCE(f) ((void)0)
+#endif
+#ifdef LGCN_EMU_STATS
+#define LGCN_EMU_COUNT_FAST() (++n_fast)
+#else
+#define LGCN_EMU_COUNT_FAST() ((void)0)
+#endif
+#ifdef LGCN_EMU_STATS
 #define EMU_STAT(k, v) \
     do { if (threadIdx.x == 0) atomicAdd(&g_emu_stats[k], (unsigned long long)(v)); } while (0)
 #else
 #define EMU_STAT(k, v) ((void)0)
 #endif
 
-// Fast-path test for one block on the chain value's bits ab (wave-uniform integer arithmetic):
-// true if the block maps ab to ab +- K[*idx] exactly. With e = binade(a), u = 2^(e-23), M = the
-// integer mantissa (a = +-M u, 2^23 <= M < 2^24) and [lo, hi] the block's bounds in units of u,
-// every trajectory value c_j = a + (c_j - a) stays in [2^e + u, 2^(e+1) - u] iff its mantissa
-// stays in [2^23 + 1, 2^24 - 1]; kSlack covers the per-step rounding drift.
-__device__ __forceinline__ bool emu_fast(uint32_t ab, int32_t lo0, int32_t hi0, int ebase,
-                                         int maxlsb, int* idx) {
-    const int E = (int)((ab >> 23) & 255u);
-    if (E == 0 || E == 255) {  // zero / subnormal / inf / NaN: sequential
-        EMU_STAT(3, 1);
-        return false;
-    }
-    const int w = E - 127 - ebase;
-    if (w < 0 || w >= kW) {
-        EMU_STAT(4, 1);
-        return false;
-    }
-    if (maxlsb >= E - 127 - 24) {  // a product may be an exact tie in this binade
-        EMU_STAT(5, 1);
-        return false;
-    }
-    const int lo = lo0 >> w;        // floor(lo0 / 2^w)
-    const int hi = -((-hi0) >> w);  // ceil(hi0 / 2^w)
-    const int M = (int)((ab & 0x7fffffu) | 0x800000u);
-    constexpr int LB = (1 << 23) + kSlack, HB = (1 << 24) - kSlack, C = 3 << 22;  // C: 1.5 * 2^23
-    const bool neg = (ab >> 31) != 0;
-    bool ok;
-    if (!neg) ok = M + lo >= LB && M + hi <= HB && C + lo >= LB && C + hi <= HB;
-    else ok = M - hi >= LB && M - lo <= HB && C - hi >= LB && C - lo <= HB;
-    *idx = 2 * w + (neg ? 1 : 0);
-    if (!ok) EMU_STAT(6, 1);
-    return ok;
-}
+// Fast-path test (k_emu_walk): with e = binade(a), u = 2^(e-23), M = the integer mantissa
+// (a = +-M u, 2^23 <= M < 2^24) and [lo, hi] the block's bounds in units of u, every trajectory
+// value a + (c_j - a) stays in [2^e + u, 2^(e+1) - u] iff its mantissa stays in
+// [2^23 + 1, 2^24 - 1]; kSlack covers the per-step rounding drift. For a < 0 the magnitude moves
+// by -[lo, hi]. The candidate's own chain (from +-1.5 * 2^e) must pass the same test.
+
+// The walk over one row for one column. Records are staged per chunk of 64 blocks: while a chunk
+// is walked, the next one's raw records are loaded into registers; at the chunk boundary they
+// go to LDS together with, for every (block, candidate), the range of start mantissas the
+// candidate's translation is valid for (the bounds test of emu_fast, precomputed in parallel
+// by all 64 lanes). Per block, the walk then needs only the chain value's exponent, sign and
+// mantissa and three words of the block's candidate row (read from LDS one block ahead).
+#define LGCN_EMU_CH 64
+
+struct EmuChunk {  // one lane's share of a chunk's raw records
+    int32_t lo, hi, pk;                 // meta of block `lane`
+    int32_t k[LGCN_EMU_CH / 2];         // translation (lane & 31) of block 2 j + (lane >> 5)
+};
 
 template <int MODE, int XD>
 __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__ edges,
@@ -370,74 +397,141 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
                                                  lgcn_epilogue_t ep) {
-    constexpr int CH = 64;  // blocks staged per chunk
-    __shared__ int32_t srel[CH * LGCN_EMU_CANDS];
+    constexpr int CH = LGCN_EMU_CH;
+    constexpr int NC = LGCN_EMU_CANDS;
+    __shared__ int32_t s_k[CH * NC], s_min[CH * NC], s_max[CH * NC];
     __shared__ float2 sq[LGCN_EMU_BLOCK];
     const int lane = threadIdx.x;
     const int c = blockIdx.y;
     const lgcn_emu_row_t er = rows[blockIdx.x];
     // the chain value, as its bits (wave-uniform)
     uint32_t ab = __float_as_uint(meta[(int64_t)er.first_block * d + c].r0);
+    auto stage_of = [&](int64_t bi) -> const float* {
+        return stage ? stage + (bi * d + c) * LGCN_EMU_BLOCK : nullptr;
+    };
+    auto load_chunk = [&](int32_t b0, EmuChunk& ck) {
+        const int nb = min(CH, er.n_blocks - b0);
+        const int64_t bl = er.first_block + b0 + min(lane, max(nb - 1, 0));
+        const int4 mv = *reinterpret_cast<const int4*>(meta + bl * d + c);
+        ck.lo = mv.x;
+        ck.hi = mv.y;
+        ck.pk = lane < nb ? mv.z : (int)0x80000000;  // past the row: identity
+        const int64_t base = (int64_t)(er.first_block + b0) * d + c;
+#pragma unroll
+        for (int j = 0; j < CH / 2; ++j) {
+            const int bb = min(2 * j + (lane >> 5), max(nb - 1, 0));
+            ck.k[j] = rel[(base + (int64_t)bb * d) * NC + (lane & 31)];
+        }
+    };
+    // chunk -> LDS: translations and, per (block, candidate k = 2 w + sign), the valid range of
+    // the start mantissa M (empty when the candidate's own chain may have left its binade)
+    auto stage_chunk = [&](const EmuChunk& ck) {
+        constexpr int LB = (1 << 23) + kSlack, HB = (1 << 24) - kSlack, C = 3 << 22;
+        const int k = lane & 31;
+        const int w = k >> 1;
+        const bool neg = k & 1;
+#pragma unroll
+        for (int j = 0; j < CH / 2; ++j) {
+            const int b = 2 * j + (lane >> 5);
+            const int32_t lo0 = __shfl(ck.lo, b);
+            const int32_t hi0 = __shfl(ck.hi, b);
+            const int lo = lo0 >> w, hi = -((-hi0) >> w);
+            const int mlo = neg ? -hi : lo, mhi = neg ? -lo : hi;  // magnitude offsets
+            const bool valid = C + mlo >= LB && C + mhi <= HB;
+            s_k[b * NC + k] = ck.k[j];
+            s_min[b * NC + k] = valid ? LB - mlo : 1 << 24;
+            s_max[b * NC + k] = valid ? HB - mhi : 0;
+        }
+    };
 #ifdef LGCN_EMU_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long n_fast = 0, n_slow = 0, t_slow = 0;
 #endif
+    EmuChunk nxt;
+    if (er.n_blocks > 1) load_chunk(1, nxt);
+    // re-run blocks come in runs: after one, the next block's data is fetched while this one
+    // runs (used if the next block is re-run too)
+    SlowData pf;
+    int64_t pf_block = -1;
     for (int32_t b0 = 1; b0 < er.n_blocks; b0 += CH) {
         const int nb = min(CH, er.n_blocks - b0);
-        // stage the chunk: lane i holds block b0+i's meta; srel[i][k] its translations
-        int32_t mlo = 0, mhi = 0, mpk = 0;
+        __syncthreads();  // the previous chunk's LDS rows are no longer read
+        stage_chunk(nxt);
+        const int32_t m_pk = nxt.pk;
+        if (b0 + CH < er.n_blocks) load_chunk(b0 + CH, nxt);  // in flight during this chunk
         __syncthreads();
-        if (lane < nb) {
-            const int64_t rc = (int64_t)(er.first_block + b0 + lane) * d + c;
-            const int4 mv = *reinterpret_cast<const int4*>(meta + rc);
-            mlo = mv.x;
-            mhi = mv.y;
-            mpk = mv.z;
-            const int4* rp = reinterpret_cast<const int4*>(rel + rc * LGCN_EMU_CANDS);
-            int4* dst = reinterpret_cast<int4*>(srel + lane * LGCN_EMU_CANDS);
-#pragma unroll
-            for (int q = 0; q < LGCN_EMU_CANDS / 4; ++q) dst[q] = rp[q];
-        }
-        __syncthreads();
-        // lane k (< 32) holds the current block's translation k, read one block ahead
-        int32_t kv = srel[lane & (LGCN_EMU_CANDS - 1)];
+        const int k = lane & 31;
+        int32_t nK = s_k[k], nMin = s_min[k], nMax = s_max[k];
         for (int i = 0; i < nb; ++i) {
-            const int32_t lo0 = __builtin_amdgcn_readlane(mlo, i);
-            const int32_t hi0 = __builtin_amdgcn_readlane(mhi, i);
-            const int32_t pk = __builtin_amdgcn_readlane(mpk, i);
-            const int32_t kcur = kv;
-            if (i + 1 < nb) kv = srel[(i + 1) * LGCN_EMU_CANDS + (lane & (LGCN_EMU_CANDS - 1))];
+            const int32_t cK = nK, cMin = nMin, cMax = nMax;
+            if (i + 1 < nb) {  // the next block's candidate row, independent of the chain value
+                nK = s_k[(i + 1) * NC + k];
+                nMin = s_min[(i + 1) * NC + k];
+                nMax = s_max[(i + 1) * NC + k];
+            }
+            const int32_t pk = __builtin_amdgcn_readlane(m_pk, i);
             const int ebase = (int)(int16_t)(pk & 0xffff);
             const int maxlsb = (int)(int16_t)(pk >> 16);
             if (maxlsb == kIdentity) {  // every product is zero: a is unchanged
                 EMU_STAT(2, 1);
                 continue;
             }
-            int idx = 0;
-            if (emu_fast(ab, lo0, hi0, ebase, maxlsb, &idx)) {
-                EMU_STAT(0, 1);
+            const int E = (int)((ab >> 23) & 255u);
+            const int w = E - 127 - ebase;
+            const int neg = (int)(ab >> 31);
+            const int idx = 2 * min(max(w, 0), kW - 1) + neg;
+            const int M = (int)((ab & 0x7fffffu) | 0x800000u);
+            const int32_t lo_m = __builtin_amdgcn_readlane(cMin, idx);
+            const int32_t hi_m = __builtin_amdgcn_readlane(cMax, idx);
+            // zero / subnormal / inf / NaN, outside the window, a possible exact tie, or a
+            // trajectory that may leave the binade: re-run the block
+            bool fast = ((unsigned)(E - 1) < 254u) & ((unsigned)w < (unsigned)kW) &
+                        (maxlsb < E - 127 - 24) & (M >= lo_m) & (M <= hi_m);
 #ifdef LGCN_EMU_STATS
-                ++n_fast;
-#endif
-                const int32_t K = __builtin_amdgcn_readlane(kcur, idx);
-                ab = (ab >> 31) ? ab - (uint32_t)K : ab + (uint32_t)K;  // same binade: mantissa add
-            } else {
-                const lgcn_emu_block_t bk = blocks[er.first_block + b0 + i];
-                EMU_STAT(1, 1);
-                EMU_STAT(7, bk.end - bk.beg);
-#ifdef LGCN_EMU_STATS
-                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-                const int64_t bi = er.first_block + b0 + i;
-                const float* st = stage ? stage + (bi * d + c) * LGCN_EMU_BLOCK : nullptr;
-                const float a = emu_slow_block<XD>(edges, bk.beg, bk.end, x, xdiv, x_nz, st, c,
-                                                   __uint_as_float(ab), sq);
-                ab = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(a));
-#ifdef LGCN_EMU_STATS
-                ++n_slow;
-                t_slow += __builtin_amdgcn_s_memtime() - t0;
-#endif
+            if (!fast) {
+                if ((unsigned)(E - 1) >= 254u) EMU_STAT(3, 1);
+                else if ((unsigned)w >= (unsigned)kW) EMU_STAT(4, 1);
+                else if (maxlsb >= E - 127 - 24) EMU_STAT(5, 1);
+                else EMU_STAT(6, 1);
             }
+#endif
+            LGCN_EMU_FORCE(fast);
+            if (fast) {
+                const int32_t K = __builtin_amdgcn_readlane(cK, idx);
+                ab = neg ? ab - (uint32_t)K : ab + (uint32_t)K;  // same binade: mantissa add
+                EMU_STAT(0, 1);
+                LGCN_EMU_COUNT_FAST();
+                continue;
+            }
+            // re-run block i as the reference does
+            const int64_t bi = er.first_block + b0 + i;
+            const lgcn_emu_block_t bk = blocks[bi];
+            EMU_STAT(1, 1);
+            EMU_STAT(7, bk.end - bk.beg);
+#ifdef LGCN_EMU_STATS
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+            SlowData sd;
+            if (pf_block == bi) sd = pf;
+            else slow_load<XD>(sd, edges, bk.beg, bk.end, x, xdiv, x_nz, stage_of(bi), c);
+            if (b0 + i + 1 < er.n_blocks) {
+                const lgcn_emu_block_t nbk = blocks[bi + 1];
+                slow_load<XD>(pf, edges, nbk.beg, nbk.end, x, xdiv, x_nz, stage_of(bi + 1), c);
+                pf_block = bi + 1;
+            }
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+            const float a = g_emu_mode == 1 ? __uint_as_float(ab)
+                                            : slow_run(sd, bk.end - bk.beg, stage != nullptr,
+                                                       __uint_as_float(ab), sq);
+#else
+            const float a = slow_run(sd, bk.end - bk.beg, stage != nullptr, __uint_as_float(ab),
+                                     sq);
+#endif
+            ab = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(a));
+#ifdef LGCN_EMU_STATS
+            ++n_slow;
+            t_slow += __builtin_amdgcn_s_memtime() - t0;
+#endif
         }
     }
 #ifdef LGCN_EMU_STATS
@@ -516,6 +610,12 @@ int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
 
 extern "C" {
 
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+int lgcn_emu_set_mode(int mode) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_mode), &mode, sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #ifdef LGCN_EMU_STATS
 // diagnostics builds only (not in lgcn.h): read and reset the walker counters
 int lgcn_emu_stats(unsigned long long* out_host) {
@@ -524,6 +624,7 @@ int lgcn_emu_stats(unsigned long long* out_host) {
     unsigned long long z[8] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
+
 
 int lgcn_emu_row_stats(unsigned long long* out_host) {  // [256][4], then reset
     if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_emu_row_stats), sizeof(g_emu_row_stats)) !=

@@ -287,6 +287,19 @@ class HubPlan:
         self.n_emu_blocks = 0 if emu_blocks is None else emu_blocks.shape[0]
         self.n_emu_rows = 0 if emu_rows is None else emu_rows.shape[0]
         self._scratch = {}
+        self._split = None
+
+    def emu_parts(self, bounds=(4096, 512)):
+        """The emulated rows cut by length into consecutive (row0, row1, block0, block1) groups:
+        rows of more than bounds[0] blocks, then more than bounds[1], then the rest (rows are
+        stored longest first). The longest walks are the critical path of a layer."""
+        if self._split is None:
+            nb = self.emu_rows[:, 2].cpu().numpy() if self.n_emu_rows else np.zeros(0, np.int64)
+            cuts = [0] + [int((nb > b).sum()) for b in bounds] + [int(nb.size)]
+            firsts = np.concatenate([[0], np.cumsum(nb)])
+            self._split = [(r0, r1, int(firsts[r0]), int(firsts[r1]))
+                           for r0, r1 in zip(cuts[:-1], cuts[1:]) if r1 > r0]
+        return self._split
 
     @property
     def n_long(self):
@@ -653,28 +666,95 @@ def _check_emb(segments, d, device):
             raise LgcnError("embedding blocks must be contiguous [rows x d]")
 
 
+_side_streams = {}
+
+
+def _side_stream(device, i=0):
+    """Per-device side streams the emulated hub rows run on, beside the layer kernel."""
+    key = (str(device), i)
+    if key not in _side_streams:
+        _side_streams[key] = torch.cuda.Stream(device)
+    return _side_streams[key]
+
+
+def emu_overlap_enabled():
+    """LGCN_EMU_OVERLAP=0 runs the emulated rows on the caller's stream, after the layer kernel
+    (lgcn_layer's order) instead of beside it on a side stream."""
+    return os.environ.get("LGCN_EMU_OVERLAP", "1") != "0"
+
+
 def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0,
-               x_nz=None):
-    """One layer Y = epilogue(Â·(X / x_div)) under the operator's hub plan (lgcn_layer: the
-    emulation block pass, the layer kernel, the chunk combine and the emulation walk).
-    x_nz: optional row bitmask of X (rows_nonzero; ADD epilogue only)."""
+               x_nz=None, kernel_events=None):
+    """One layer Y = epilogue(Â·(X / x_div)) under the operator's hub plan: the emulation block
+    pass, the layer kernel (bundles, long rows, chunks), the chunk combine and the emulation
+    walk. The emulated rows touch no row the layer kernel writes, so by default they run on a
+    side stream concurrently with it (forked from and joined back into the caller's stream:
+    graph-capture safe); LGCN_EMU_OVERLAP=0 serialises them (lgcn_layer).
+    x_nz: optional row bitmask of X (rows_nonzero; ADD epilogue only). kernel_events: optional
+    (start, end) torch.cuda.Event pair recorded on the caller's stream around the layer kernel
+    launch (lgcn_layer: bundles, long rows, chunks) — bench.py's live timing of that kernel."""
     lib = load_library()
     hp = hubs or graph.hubs(hub_threshold)
     stream = stream or _stream(graph.device)
     plan = hp.struct(d, graph.device)
     x = rows_desc(x_segments, d)
-    _check(lib.lgcn_layer(_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids),
-                          graph.n_rows, ctypes.byref(plan), x, x_div, _ptr(x_nz), _ptr(y),
-                          y.stride(0), d, ctypes.byref(epi), stream), "lgcn_layer")
+    args = (_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), graph.n_rows)
+    if not (hp.n_emu_rows and emu_overlap_enabled()):
+        if kernel_events is not None:
+            kernel_events[0].record()
+        _check(lib.lgcn_layer(*args, ctypes.byref(plan), x, x_div, _ptr(x_nz), _ptr(y),
+                              y.stride(0), d, ctypes.byref(epi), stream), "lgcn_layer")
+        if kernel_events is not None:
+            kernel_events[1].record()
+        return y
+    main = torch.cuda.current_stream(graph.device)
+    if main.cuda_stream != (stream.value or 0):
+        raise LgcnError("spmm_layer: stream must be the device's current stream")
+    # the longest rows' walks are the critical path: their block pass runs first, alone, and
+    # their walk starts as soon as it is done, on a side stream of their own; shorter emulated
+    # rows follow on further side streams (rows are stored longest first)
+    parts = hp.emu_parts()
+    sides = [_side_stream(graph.device, i) for i in range(len(parts))]
+    for sd in sides:
+        sd.wait_stream(main)        # X (and the epilogue operands) are ready
+    rb, bb = hp.emu_rows.element_size() * 4, hp.emu_blocks.element_size() * 4
+    for sd, (r0, r1, b0, b1) in zip(sides, parts):
+        if r1 <= r0:
+            continue
+        ss = ctypes.c_void_p(sd.cuda_stream)
+        # records are indexed by block: a sub-range of blocks writes at its own offset
+        _check(lib.lgcn_emu_blocks(
+            _ptr(graph.edges), plan.emu_blocks + b0 * bb, b1 - b0, x, x_div, _ptr(x_nz), d,
+            plan.emu_rel + b0 * d * LGCN_EMU_CANDS * 4, plan.emu_meta + b0 * d * LGCN_EMU_META_BYTES,
+            plan.emu_stage + b0 * d * LGCN_EMU_BLOCK * 4 if plan.emu_stage else None, ss),
+            "lgcn_emu_blocks")
+    rest = PlanT.from_buffer_copy(plan)
+    rest.n_emu_rows = rest.n_emu_blocks = 0
+    if kernel_events is not None:
+        kernel_events[0].record()
+    _check(lib.lgcn_layer(*args, ctypes.byref(rest), x, x_div, _ptr(x_nz), _ptr(y), y.stride(0),
+                          d, ctypes.byref(epi), stream), "lgcn_layer")
+    if kernel_events is not None:
+        kernel_events[1].record()
+    for sd, (r0, r1, b0, b1) in zip(sides, parts):
+        if r1 <= r0:
+            continue
+        _check(lib.lgcn_emu_walk(_ptr(graph.edges), plan.emu_blocks, plan.emu_rows + r0 * rb,
+                                 r1 - r0, plan.emu_rel, plan.emu_meta, plan.emu_stage, x, x_div,
+                                 _ptr(x_nz), _ptr(y), y.stride(0), d, ctypes.byref(epi),
+                                 ctypes.c_void_p(sd.cuda_stream)), "lgcn_emu_walk")
+    for sd in sides:
+        main.wait_stream(sd)        # every row of Y written
     return y
 
 
 def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
-                      return_layers=False, hub_mode=None, emu_min=None):
+                      return_layers=False, hub_mode=None, emu_min=None, kernel_events=None):
     """final = mean(E0, Â E0, ..., Â^K E0) with E0 = cat(segments) (never materialised).
 
-    layer_events: optional list of (start, end) torch.cuda.Event pairs recorded around each
-    layer's lgcn_spmm_layer launch on the current stream (bench.py's live kernel timing).
+    layer_events: optional list of (start, end) torch.cuda.Event pairs recorded on the current
+    stream around each whole layer (every stream of it joined); kernel_events: the same around
+    each layer's layer-kernel launch alone (spmm_layer) — bench.py's live timing.
     """
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
@@ -706,7 +786,8 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
                                div=float(K + 1))
             if layer_events is not None:
                 layer_events[k - 1][0].record()
-            spmm_layer(graph, xs, y, d, ep, hub_threshold, hp, stream)
+            spmm_layer(graph, xs, y, d, ep, hub_threshold, hp, stream,
+                       kernel_events=None if kernel_events is None else kernel_events[k - 1])
             if layer_events is not None:
                 layer_events[k - 1][1].record()
         return (out, layers) if return_layers else out

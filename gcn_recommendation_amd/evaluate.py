@@ -91,10 +91,34 @@ def topk_fused(user_emb, item_emb, users, mask_rowptr, mask_items, k=20):
     return top_s[:n], top_i[:n]
 
 
+FUSED_DIMS = (64, 128)   # lgcn_score_topk's widths (include/lgcn.h)
+FUSED_MAX_K = 32
+
+
+def fused_supported(d, k):
+    return d in FUSED_DIMS and 1 <= k <= FUSED_MAX_K
+
+
+def topk_torch(user_emb, item_emb, users, mask_rowptr, mask_items, k=20):
+    """main.py:420-426 as torch ops for any d and k: scores = user rows · item tableᵀ, every
+    training item of the user set to -1e10, topk(k)."""
+    dev = item_emb.device
+    users = np.asarray(users, dtype=np.int64)
+    scores = torch.matmul(user_emb[torch.from_numpy(users).to(dev)], item_emb.T)
+    lens = mask_rowptr[users + 1] - mask_rowptr[users]
+    if lens.sum():
+        rr = np.repeat(np.arange(len(users)), lens)
+        cc = np.concatenate([mask_items[mask_rowptr[u]:mask_rowptr[u + 1]] for u in users])
+        scores[torch.from_numpy(rr).to(dev), torch.from_numpy(cc.astype(np.int64)).to(dev)] = -1e10
+    return torch.topk(scores, k=k)
+
+
 def evaluate(model, val_or_test_data, train_data, norm_adj_tensor, k, device, batch_size=8192,
              use_brand=True, item_brand_df=None):
-    """main.py:404-439 (same signature and metrics) on the fused kernel: one propagation, then
-    per batch of users one lgcn_score_topk launch; hit -> recall 1, NDCG = 1/log2(pos + 2)."""
+    """main.py:404-439 (same signature and metrics): one propagation, then per batch of users
+    one lgcn_score_topk launch (fused score + mask + top-k) when the width and k are ones the
+    kernel has (d in FUSED_DIMS, k <= FUSED_MAX_K), torch matmul + mask + topk otherwise — the
+    reference works for any d and k, so does this; hit -> recall 1, NDCG = 1/log2(pos + 2)."""
     model.eval()
     test_user_items = dict(zip(val_or_test_data["user_idx"], val_or_test_data["item_idx"]))
     test_users = np.fromiter(test_user_items.keys(), dtype=np.int64, count=len(test_user_items))
@@ -103,10 +127,14 @@ def evaluate(model, val_or_test_data, train_data, norm_adj_tensor, k, device, ba
         all_user_emb, all_item_emb, _, _, _ = model(norm_adj_tensor)
         mrow, mit = mask_csr(train_data["user_idx"].to_numpy(), train_data["item_idx"].to_numpy(),
                              all_user_emb.shape[0])
+        fused = fused_supported(all_item_emb.shape[1], k) and all_item_emb.is_cuda
         tops = []
         for s in range(0, len(test_users), batch_size):
-            _, ti = topk_fused(all_user_emb, all_item_emb, test_users[s:s + batch_size], mrow,
-                               mit, k)
+            bu = test_users[s:s + batch_size]
+            if fused:
+                _, ti = topk_fused(all_user_emb, all_item_emb, bu, mrow, mit, k)
+            else:
+                _, ti = topk_torch(all_user_emb, all_item_emb, bu, mrow, mit, k)
             tops.append(ti.cpu().numpy())
     top = np.concatenate(tops) if tops else np.zeros((0, k), np.int32)
     hit = top == truth[:, None]

@@ -49,7 +49,7 @@ class LightGCN(nn.Module):
         """(final_user, final_item, final_brand) blocks."""
         if adj_mat.device.type == "cuda":
             final = engine.propagate_blocks(adj_mat, segments, self.n_layers)
-            if self.debug:
+            if self.debug and self.n_layers > 0:  # lightgcn.py:44-51 prints once per layer
                 with torch.no_grad():
                     _, layers = engine.propagate_forward(
                         engine.graph_from_coo(adj_mat), [s.detach() for s in segments],

@@ -147,14 +147,19 @@ def forward_f64(rows, cols, vals, e0, K):
     return out
 
 
-def reference_forward_torch(adj, ego, K):
-    """models/lightgcn.py:41-54 with torch CPU ops, exactly as the reference runs them."""
+def reference_forward_torch(adj, ego, K, layer_times=None):
+    """models/lightgcn.py:41-54 with torch CPU ops, exactly as the reference runs them.
+    layer_times: optional list that receives each torch.sparse.mm's wall seconds."""
+    import time
     import torch
     with torch.no_grad():
         all_e = [ego]
         x = ego
         for _ in range(K):
+            t0 = time.perf_counter()
             x = torch.sparse.mm(adj, x)
+            if layer_times is not None:
+                layer_times.append(time.perf_counter() - t0)
             all_e.append(x)
         return torch.mean(torch.stack(all_e, dim=0), dim=0)
 

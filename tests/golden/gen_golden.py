@@ -8,7 +8,7 @@ graphs, and dumps inputs + outputs as `.npz` data fixtures next to this file. On
 reference: edge lists, the normalised adjacency it built, embeddings, gradients, losses, metrics.
 
 Run (in the build container only; the GPU box has no /root/reference):
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [debug]
 """
 import contextlib
 import io
@@ -163,6 +163,56 @@ def make_case(name, users, items, U, I, B, item_brand, d, K, use_brand, fusion_c
     print(f"{name}: N={U + I + B} nnz={len(vals)} d={d} K={K} recall={rec:.4f} ndcg={ndcg:.4f}")
 
 
+def make_debug_case(name, users, items, U, I, B, item_brand, d, K, use_brand):
+    """config.debug=True forward (lightgcn.py:49-51 per-layer brand norms, :62-78 cosine check
+    and its torch.manual_seed(42) side effect): the printed lines and the CPU generator's next
+    draws after the forward."""
+    ref_main, LightGCN, _ = _import_reference()
+    rng = np.random.default_rng(123)
+    test_items = rng.integers(0, I, U)
+    with tempfile.TemporaryDirectory() as tmp:
+        _write_dataset(tmp, users, items, test_items, item_brand, U, I, B)
+        with contextlib.redirect_stdout(io.StringIO()):
+            tr, va, te, nu, ni, nb, adj, ibdf = ref_main.load_preprocessed_data(
+                tmp, "cpu", use_brand=use_brand, debug=False)
+    idx = adj._indices().numpy()
+    cfg = _Cfg(d, K)
+    cfg.debug = True
+    torch.manual_seed(42)
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = LightGCN(nu, ni, nb, cfg)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        fu, fi, fb, _, _ = model(adj, use_brand=use_brand)
+    out = {
+        "U": np.int64(U), "I": np.int64(I), "B": np.int64(B), "d": np.int64(d), "K": np.int64(K),
+        "use_brand": np.int64(int(use_brand)),
+        "train_user": tr["user_idx"].to_numpy().astype(np.int64),
+        "train_item": tr["item_idx"].to_numpy().astype(np.int64),
+        "ib_item": np.asarray(item_brand[0], dtype=np.int64),
+        "ib_brand": np.asarray(item_brand[1], dtype=np.int64),
+        "adj_row": idx[0].astype(np.int32), "adj_col": idx[1].astype(np.int32),
+        "adj_val": adj._values().numpy(),
+        "stdout": np.array(buf.getvalue()),
+        "rng_after": torch.rand(8).numpy(),
+    }
+    _keep(out, "final", torch.cat([fu, fi, fb]).detach().numpy())
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+    print(f"{name}: debug stdout {len(buf.getvalue().splitlines())} lines")
+
+
+def main_debug():
+    rng = np.random.default_rng(0)
+    U, I, E = 1000, 1000, 10000
+    u = rng.integers(0, U, E)
+    it = rng.integers(0, I, E)
+    brands = np.random.default_rng(1).integers(0, 50, I)
+    make_debug_case("debug_c1_brand", u, it, U, I, 50, (np.arange(I), brands), 64, 2,
+                    use_brand=True)
+    make_debug_case("debug_c1_brand_k0", u, it, U, I, 50, (np.arange(I), brands), 64, 0,
+                    use_brand=True)
+
+
 def main():
     torch.set_num_threads(1)
     # C1 (BASELINE.json configs[0]): 1k x 1k x 10k uniform, default_rng(0), d=64, K=2
@@ -199,4 +249,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    # `gen_golden.py debug` writes only the debug-diagnostics fixtures
+    main_debug() if sys.argv[1:] == ["debug"] else main()

@@ -28,9 +28,11 @@ def stats(lib):
     return dict(zip(NAMES, list(buf)))
 
 
-def row_stats(lib, hp, d):
+def row_stats(lib, hp, d, quiet=False):
     buf = (ctypes.c_ulonglong * 1024)()
     assert lib.lgcn_emu_row_stats(buf) == 0
+    if quiet:
+        return
     a = np.array(buf, dtype=np.float64).reshape(256, 4)
     rows = hp.emu_rows.cpu().numpy()
     for k in list(range(min(8, len(rows)))) + [min(len(rows), 256) - 1]:
@@ -58,6 +60,7 @@ def main():
     if a.stats:
         lib.lgcn_emu_stats.argtypes = [ctypes.c_void_p]
         lib.lgcn_emu_row_stats.argtypes = [ctypes.c_void_p]
+        lib.lgcn_emu_set_mode.argtypes = [ctypes.c_int]
     r, c, v, _, _, _ = bench.make_graph(cfg, a.gen, 16)
     U, I, B = cfg["users"], cfg["items"], cfg.get("brands", 0)
     n, d, K = U + I + B, cfg["d"], cfg["K"]
@@ -84,16 +87,38 @@ def main():
         if a.stats:
             print("  walker decisions (all layers):", stats(lib), flush=True)
             row_stats(lib, hp, d)
+    if a.stats:
+        per_layer_stats(lib, g, segs, d, K, a.thr, a.emu_min, hp)
     if a.walk:
         walk_timing(g, segs, d, a.thr, a.emu_min)
 
 
 
 
+def per_layer_stats(lib, g, segs, d, K, thr, emu_min, hp):
+    """Walker decisions of each layer of one forward (row 0 and all rows)."""
+    n = g.n_rows
+    stats(lib)
+    row_stats(lib, hp, d, quiet=True)
+    layers = [torch.empty((n, d), device=g.device) for _ in range(K)]
+    xs = segs
+    for k in range(K):
+        engine.spmm_layer(g, xs, layers[k], d, engine._epilogue(engine.LGCN_EPI_STORE), thr,
+                          hubs=g.hubs(thr, mode="exact", emu_min=emu_min))
+        torch.cuda.synchronize()
+        st = stats(lib)
+        buf = (ctypes.c_ulonglong * 1024)()
+        lib.lgcn_emu_row_stats(buf)
+        r0 = np.array(buf[:4], dtype=np.float64)
+        print(f"  layer {k + 1}: all rows {st}; row 0 fast {r0[0] / d:.0f} slow {r0[1] / d:.0f} "
+              f"per column", flush=True)
+        xs = [layers[k]]
+
+
 def walk_timing(g, segs, d, thr, emu_min):
     """Layer 1's emulation walk timed on subsets of the emulated rows (isolated critical path
-    vs the crowd)."""
-    import ctypes as C
+    vs the crowd); with a LGCN_EMU_STATS build also row 0's decisions and the timing
+    experiments (1: re-run blocks skip their chain, 2: every block translates)."""
     lib = engine.load_library()
     hp = g.hubs(thr, mode="exact", emu_min=emu_min)
     plan = hp.struct(d, g.device)
@@ -103,17 +128,34 @@ def walk_timing(g, segs, d, thr, emu_min):
     ep = engine._epilogue(engine.LGCN_EPI_STORE)
     assert lib.lgcn_emu_blocks(engine._ptr(g.edges), plan.emu_blocks, hp.n_emu_blocks, x, 1.0, None,
                                d, plan.emu_rel, plan.emu_meta, plan.emu_stage, st) == 0
-    rows = hp.emu_rows
-    for lo, hi in ((0, 1), (1, 2), (0, 8), (8, hp.n_emu_rows), (0, hp.n_emu_rows)):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        assert lib.lgcn_emu_walk(engine._ptr(g.edges), plan.emu_blocks, rows[lo:].data_ptr(),
-                                 hi - lo, plan.emu_rel, plan.emu_meta, plan.emu_stage, x, 1.0,
-                                 None, engine._ptr(y), d, d, C.byref(ep), st) == 0
-        b.record()
-        torch.cuda.synchronize()
-        print(f"  walk rows [{lo}, {hi}): {a.elapsed_time(b):.3f} ms", flush=True)
-
+    has_modes = bool(os.environ.get("LGCN_LIB")) and hasattr(lib, "lgcn_emu_set_mode")
+    has_stats = has_modes and hasattr(lib, "lgcn_emu_stats")
+    if has_modes:
+        lib.lgcn_emu_set_mode.argtypes = [ctypes.c_int]
+    for mode in ([0, 1, 2] if has_modes else [0]):
+        if has_modes:
+            lib.lgcn_emu_set_mode(mode)
+            torch.cuda.synchronize()
+        if has_stats:
+            stats(lib)
+            row_stats(lib, hp, d, quiet=True)
+        if has_modes:
+            print(f" walker mode {mode} (0 normal, 1 re-run blocks skip the chain, 2 all translate)")
+        for lo, hi in ((0, 1), (1, 2), (0, 8), (8, hp.n_emu_rows), (0, hp.n_emu_rows)):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            assert lib.lgcn_emu_walk(engine._ptr(g.edges), plan.emu_blocks,
+                                     hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
+                                     plan.emu_meta, plan.emu_stage, x, 1.0, None, engine._ptr(y),
+                                     d, d, ctypes.byref(ep), st) == 0
+            b.record()
+            torch.cuda.synchronize()
+            print(f"  walk rows [{lo}, {hi}): {a.elapsed_time(b):.3f} ms", flush=True)
+            if has_stats and (lo, hi) == (0, 1):
+                print("   row 0 decisions:", stats(lib), flush=True)
+                row_stats(lib, hp, d, quiet=True)
+    if has_modes:
+        lib.lgcn_emu_set_mode(0)
 
 if __name__ == "__main__":
     main()
