@@ -142,7 +142,10 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     // one sub-window: steps past the block end read as (0, 0), and fma(0, 0, c) == c for every
     // chain value (a chain is never -0), so the unrolled steps need no guard
     // this (block, column)'s elements, in step order (the walk re-runs a block from here)
-    float* st = stage ? stage + ((int64_t)blockIdx.x * d + cc) * LGCN_EMU_BLOCK : nullptr;
+    // stage layout [block][d + 1][BLOCK]: column c's X elements, then (column d) the edge values
+    float* st = stage ? stage + ((int64_t)blockIdx.x * (d + 1) + cc) * LGCN_EMU_BLOCK : nullptr;
+    float* sv = stage && blockIdx.y == 0
+                    ? stage + ((int64_t)blockIdx.x * (d + 1) + d) * LGCN_EMU_BLOCK : nullptr;
     auto stage_sub = [&](const float (&xv)[SW], int step0) {
         if (!st || !act) return;
 #pragma unroll
@@ -195,6 +198,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     for (int32_t j0 = blk.beg; j0 < blk.end; j0 += 64) {
         const int n = min(64, blk.end - j0);
         const int2 nrec = load_rec(j0 + 64);  // next window's records, in flight meanwhile
+        if (sv) sv[j0 - blk.beg + lane] = __int_as_float(rec.y);  // (0 past the block end)
         float xa[SW], va[SW], xb[SW], vb[SW];
         // the loads of sub-window k + 1 are issued before sub-window k is computed
         const int w0 = j0 - blk.beg;
@@ -284,11 +288,17 @@ __device__ __forceinline__ void slow_load(SlowData& sd, const lgcn_edge_t* __res
     }
 }
 
-__device__ __forceinline__ float slow_run(const SlowData& sd, int n, bool staged, float a,
-                                          float2* sq) {
+// LDS ordering point for the walker (a one-wave workgroup: a wave's LDS operations complete in
+// order, so only the compiler must not move LDS accesses across this point). __syncthreads()
+// would also make the compiler drain every global load in flight (vmcnt(0)) — the prefetched
+// re-run blocks and the next chunk's records — exposing their latency at every re-run block.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// A re-run block's (val, x) pairs from a SlowData slot to LDS (sq[step] = (val, x)).
+__device__ __forceinline__ void slow_stage(const SlowData& sd, int n, bool staged, float2* sq) {
     constexpr int Q = LGCN_EMU_BLOCK / 64;
     const int lane = threadIdx.x;
-    __syncthreads();  // the previous chain's reads of sq are done
+    wave_lds_sync();  // the previous chain's reads of sq are done
 #pragma unroll
     for (int t = 0; t < Q; ++t) {
         const bool in = t * 64 + lane < n;
@@ -296,13 +306,17 @@ __device__ __forceinline__ float slow_run(const SlowData& sd, int n, bool staged
                                         staged ? 0.f : sd.xg[t]);
     }
     if (staged) {
-        __syncthreads();
+        wave_lds_sync();
         const float xv[4] = {sd.xs.x, sd.xs.y, sd.xs.z, sd.xs.w};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             if (4 * lane + t < n) sq[4 * lane + t].y = xv[t];
     }
-    __syncthreads();
+    wave_lds_sync();
+}
+
+// The sequential chain over a staged block: a = fma(val_j, x_j, a), j = 0 .. n-1.
+__device__ __forceinline__ float slow_chain(int n, float a, const float2* sq) {
     int i = 0;
     if (n == LGCN_EMU_BLOCK) {
         // full block: the LDS reads run PF groups of 8 steps ahead of the FMAs, so only the
@@ -357,9 +371,16 @@ __device__ int g_emu_mode;
 #define LGCN_EMU_FORCE(f) ((void)0)
 #endif
 #ifdef LGCN_EMU_STATS
-#define LGCN_EMU_COUNT_FAST() (++n_fast)
+// phase timer of the walker wave (row 0, column 0): s_memtime deltas per phase, then counts
+// [stage, predict, fetch+wait, scans, chains, on-demand fetch, -, -, chunks, predicted, re-run,
+//  not predicted]
+__device__ unsigned long long g_emu_phase[16];
+#define PH_MARK(k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+                        ph[k] += now_ - ph_last; ph_last = now_; } while (0)
+#define PH_COUNT(k, v) (ph[k] += (v))
 #else
-#define LGCN_EMU_COUNT_FAST() ((void)0)
+#define PH_MARK(k) ((void)0)
+#define PH_COUNT(k, v) ((void)0)
 #endif
 #ifdef LGCN_EMU_STATS
 #define EMU_STAT(k, v) \
@@ -374,18 +395,97 @@ __device__ int g_emu_mode;
 // [2^23 + 1, 2^24 - 1]; kSlack covers the per-step rounding drift. For a < 0 the magnitude moves
 // by -[lo, hi]. The candidate's own chain (from +-1.5 * 2^e) must pass the same test.
 
-// The walk over one row for one column. Records are staged per chunk of 64 blocks: while a chunk
-// is walked, the next one's raw records are loaded into registers; at the chunk boundary they
-// go to LDS together with, for every (block, candidate), the range of start mantissas the
-// candidate's translation is valid for (the bounds test of emu_fast, precomputed in parallel
-// by all 64 lanes). Per block, the walk then needs only the chain value's exponent, sign and
-// mantissa and three words of the block's candidate row (read from LDS one block ahead).
+// The walk over one row for one column, 64 blocks at a time. Records are staged per chunk of 64
+// blocks: while a chunk is walked, the next one's raw records are loaded into registers; at the
+// chunk boundary they go to LDS together with, for every (block, candidate), the range of start
+// mantissas the candidate's translation is valid for (the bounds test above, precomputed by all
+// 64 lanes). Within a chunk the walk is a SPECULATIVE SCAN: with the chain value's binade, sign
+// and mantissa (E, s, M) fixed, lane i takes block i's translation for (E, s), an exclusive
+// prefix sum over the lanes gives the mantissa block i starts from if every block before it
+// translates, and each lane tests its own block at that start. Up to the first failing block f
+// every block translates, so the prefix at f is exactly what a block-by-block walk computes; f
+// is re-run as the sequential chain and the scan resumes after it. A chunk of fast blocks costs
+// one scan instead of 64 dependent steps.
+// Re-run blocks need their (val, x) pairs, a global-memory round trip each. They are PREDICTED
+// per chunk before the walk: the same scan run with approximate continuation (after a failing
+// block f the value is taken as a + T_f, block f's chain from +0 — the true value to within its
+// rounding) names the blocks likely to fail; their staged edge values and X elements go straight
+// to LDS slots by LDS-DMA (global_load_lds_dwordx4) in one batch, so a chunk waits for memory
+// once.
+// A block that fails without having been predicted is fetched on demand into a spare slot.
 #define LGCN_EMU_CH 64
+#define LGCN_EMU_SLOTS 15   // predicted re-run blocks per chunk with LDS slots (+1 spare)
 
 struct EmuChunk {  // one lane's share of a chunk's raw records
     int32_t lo, hi, pk;                 // meta of block `lane`
+    float t;                            // its chain from +0 (EmuMeta::r0)
     int32_t k[LGCN_EMU_CH / 2];         // translation (lane & 31) of block 2 j + (lane >> 5)
 };
+
+// Inclusive prefix sum over the 64 lanes of a wave by DPP row shifts and row broadcasts (no LDS
+// round trips: the walker's scan is on its critical path).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// A block's staged edge values and X elements -> an LDS slot by LDS-DMA
+// (global_load_lds_dwordx4: the LDS destination is base + lane * 16 B; both sources are 1 KB,
+// 1 KB-aligned rows of the stage).
+__device__ __forceinline__ void fetch_block_lds(const float* __restrict__ sv,
+                                                const float* __restrict__ sx, float* v, float* xs) {
+    const int lane = threadIdx.x;
+    __builtin_amdgcn_global_load_lds(sv + 4 * lane, v, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(sx + 4 * lane, xs, 16, 0, 0);
+}
+
+// The sequential chain over a block held in an LDS slot: a = fma(v_j, x_j, a), j < n.
+__device__ __forceinline__ float slot_chain(int n, float a, const float* __restrict__ v,
+                                            const float* __restrict__ xs) {
+    if (n == LGCN_EMU_BLOCK) {
+        // full block: the LDS reads run PF groups of 8 steps ahead of the FMAs, so only the
+        // dependent FMA chain is on the critical path
+        constexpr int NG = LGCN_EMU_BLOCK / 8, PF = 4;
+        float4 wv[PF][2], wx[PF][2];
+#pragma unroll
+        for (int g = 0; g < PF; ++g) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                wv[g][k] = reinterpret_cast<const float4*>(v + 8 * g)[k];
+                wx[g][k] = reinterpret_cast<const float4*>(xs + 8 * g)[k];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const float4 cv = wv[g % PF][k], cx = wx[g % PF][k];
+                a = __builtin_fmaf(cv.x, cx.x, a);
+                a = __builtin_fmaf(cv.y, cx.y, a);
+                a = __builtin_fmaf(cv.z, cx.z, a);
+                a = __builtin_fmaf(cv.w, cx.w, a);
+            }
+            if (g + PF < NG) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    wv[g % PF][k] = reinterpret_cast<const float4*>(v + 8 * (g + PF))[k];
+                    wx[g % PF][k] = reinterpret_cast<const float4*>(xs + 8 * (g + PF))[k];
+                }
+            }
+            // keep the reads PF groups ahead (the scheduler would otherwise sink them next to
+            // their use and wait for each group's LDS round trip)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return a;
+    }
+    for (int i = 0; i < n; ++i) a = __builtin_fmaf(v[i], xs[i], a);
+    return a;
+}
 
 template <int MODE, int XD>
 __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__ edges,
@@ -399,15 +499,19 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                                                  lgcn_epilogue_t ep) {
     constexpr int CH = LGCN_EMU_CH;
     constexpr int NC = LGCN_EMU_CANDS;
+    constexpr int NS = LGCN_EMU_SLOTS;
+    static_assert(CH == 64, "one lane per block of a chunk");
     __shared__ int32_t s_k[CH * NC], s_min[CH * NC], s_max[CH * NC];
-    __shared__ float2 sq[LGCN_EMU_BLOCK];
+    __shared__ float s_v[NS + 1][LGCN_EMU_BLOCK];    // re-run blocks' edge values
+    __shared__ float s_xs[NS + 1][LGCN_EMU_BLOCK];   // ... and their X elements
+    __shared__ float2 sq[LGCN_EMU_BLOCK];            // no-stage mode: gathered (val, x)
     const int lane = threadIdx.x;
     const int c = blockIdx.y;
     const lgcn_emu_row_t er = rows[blockIdx.x];
     // the chain value, as its bits (wave-uniform)
     uint32_t ab = __float_as_uint(meta[(int64_t)er.first_block * d + c].r0);
     auto stage_of = [&](int64_t bi) -> const float* {
-        return stage ? stage + (bi * d + c) * LGCN_EMU_BLOCK : nullptr;
+        return stage ? stage + (bi * (d + 1) + c) * LGCN_EMU_BLOCK : nullptr;
     };
     auto load_chunk = [&](int32_t b0, EmuChunk& ck) {
         const int nb = min(CH, er.n_blocks - b0);
@@ -416,6 +520,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         ck.lo = mv.x;
         ck.hi = mv.y;
         ck.pk = lane < nb ? mv.z : (int)0x80000000;  // past the row: identity
+        ck.t = __int_as_float(mv.w);
         const int64_t base = (int64_t)(er.first_block + b0) * d + c;
 #pragma unroll
         for (int j = 0; j < CH / 2; ++j) {
@@ -443,98 +548,144 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
             s_max[b * NC + k] = valid ? HB - mhi : 0;
         }
     };
+    // block k of the row holds edges [row_beg + k * BLOCK, min(.. + BLOCK, row_end)) (plan_emulation)
+    const int32_t row_beg = blocks[er.first_block].beg;
+    const int32_t row_end = blocks[er.first_block + er.n_blocks - 1].end;
+    auto fetch_slot = [&](int32_t kb, int s) {
+        const int64_t bi = er.first_block + kb;
+        fetch_block_lds(stage + (bi * (d + 1) + d) * LGCN_EMU_BLOCK, stage_of(bi), s_v[s],
+                        s_xs[s]);
+    };
 #ifdef LGCN_EMU_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long n_fast = 0, n_slow = 0, t_slow = 0;
+    unsigned long long ph[16] = {0};
+    unsigned long long ph_last = t_start;
 #endif
     EmuChunk nxt;
     if (er.n_blocks > 1) load_chunk(1, nxt);
-    // re-run blocks come in runs: after one, the next block's data is fetched while this one
-    // runs (used if the next block is re-run too)
-    SlowData pf;
-    int64_t pf_block = -1;
     for (int32_t b0 = 1; b0 < er.n_blocks; b0 += CH) {
         const int nb = min(CH, er.n_blocks - b0);
-        __syncthreads();  // the previous chunk's LDS rows are no longer read
+        wave_lds_sync();  // the previous chunk's LDS rows and slots are no longer read
         stage_chunk(nxt);
-        const int32_t m_pk = nxt.pk;
+        const int my_eb = (int)(int16_t)(nxt.pk & 0xffff);   // lane i: block i's ebase,
+        const int my_ml = (int)(int16_t)(nxt.pk >> 16);      // maxlsb,
+        const float my_t = nxt.t;                            // and chain from +0
+        const bool my_id = my_ml == kIdentity;  // every product zero: translation by 0
+        wave_lds_sync();
+        PH_MARK(0);
+        PH_COUNT(8, 1);
+        // The speculative test from block `from` with chain value bits `a`: lane i's start
+        // mantissa if every block in [from, i) translates (exclusive prefix of the mantissa
+        // changes), and the mask of blocks that cannot translate from there. `incl` returns the
+        // inclusive prefix, `dm` the lane's own change.
+        auto test = [&](uint32_t a, int from, int& incl, int& dm) -> unsigned long long {
+            const int E = (int)((a >> 23) & 255u);
+            const int neg = (int)(a >> 31);
+            const int M = (int)((a & 0x7fffffu) | 0x800000u);
+            const int w = E - 127 - my_eb;
+            const int idx = lane * NC + 2 * min(max(w, 0), kW - 1) + neg;
+            const int32_t K = s_k[idx], mn = s_min[idx], mx = s_max[idx];
+            const bool act = lane < nb && lane >= from;
+            dm = act && !my_id ? (neg ? -K : K) : 0;  // |K| < 2^24: the sums fit in int32
+            incl = wave_incl_scan(dm);
+            const int start = M + incl - dm;
+            bool ok = my_id || (((unsigned)(E - 1) < 254u) & ((unsigned)w < (unsigned)kW) &
+                                (my_ml < E - 127 - 24) & (start >= mn) & (start <= mx));
+            LGCN_EMU_FORCE(ok);
+            return __ballot(act && !ok);
+        };
+        // predicted re-run blocks of this chunk (stage mode: their data goes to LDS slots)
+        unsigned long long pred = 0;
+        if (stage) {
+            uint32_t pa = ab;
+            int from = 0;
+            for (int it = 0; it < NS && from < nb; ++it) {
+                int incl, dm;
+                const unsigned long long bad = test(pa, from, incl, dm);
+                if (!bad) break;
+                const int f = (int)__builtin_ctzll(bad);
+                pred |= 1ull << f;
+                pa += (uint32_t)__builtin_amdgcn_readlane(incl - dm, f);
+                pa = __float_as_uint(__uint_as_float(pa) + __int_as_float(
+                         __builtin_amdgcn_readlane(__float_as_int(my_t), f)));
+                from = f + 1;
+            }
+        }
+        PH_MARK(1);
+        PH_COUNT(9, __builtin_popcountll(pred));
         if (b0 + CH < er.n_blocks) load_chunk(b0 + CH, nxt);  // in flight during this chunk
-        __syncthreads();
-        const int k = lane & 31;
-        int32_t nK = s_k[k], nMin = s_min[k], nMax = s_max[k];
-        for (int i = 0; i < nb; ++i) {
-            const int32_t cK = nK, cMin = nMin, cMax = nMax;
-            if (i + 1 < nb) {  // the next block's candidate row, independent of the chain value
-                nK = s_k[(i + 1) * NC + k];
-                nMin = s_min[(i + 1) * NC + k];
-                nMax = s_max[(i + 1) * NC + k];
-            }
-            const int32_t pk = __builtin_amdgcn_readlane(m_pk, i);
-            const int ebase = (int)(int16_t)(pk & 0xffff);
-            const int maxlsb = (int)(int16_t)(pk >> 16);
-            if (maxlsb == kIdentity) {  // every product is zero: a is unchanged
-                EMU_STAT(2, 1);
-                continue;
-            }
-            const int E = (int)((ab >> 23) & 255u);
-            const int w = E - 127 - ebase;
-            const int neg = (int)(ab >> 31);
-            const int idx = 2 * min(max(w, 0), kW - 1) + neg;
-            const int M = (int)((ab & 0x7fffffu) | 0x800000u);
-            const int32_t lo_m = __builtin_amdgcn_readlane(cMin, idx);
-            const int32_t hi_m = __builtin_amdgcn_readlane(cMax, idx);
-            // zero / subnormal / inf / NaN, outside the window, a possible exact tie, or a
-            // trajectory that may leave the binade: re-run the block
-            bool fast = ((unsigned)(E - 1) < 254u) & ((unsigned)w < (unsigned)kW) &
-                        (maxlsb < E - 127 - 24) & (M >= lo_m) & (M <= hi_m);
+        if (pred) {
+            int s = 0;
+            for (unsigned long long m = pred; m; m &= m - 1, ++s)
+                fetch_slot(b0 + (int)__builtin_ctzll(m), s);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slots (and the next chunk) landed
+        }
+        PH_MARK(2);
+        // lane i: the slot holding block i's data, or -1
+        const int my_slot = ((pred >> lane) & 1ull)
+            ? (int)__builtin_popcountll(pred & ((1ull << lane) - 1ull)) : -1;
+        int from = 0;
+        while (true) {
+            int incl, dm;
+            const unsigned long long bad = test(ab, from, incl, dm);
+            const int f = bad ? (int)__builtin_ctzll(bad) : nb;
+            // blocks [from, f) translate: their mantissa changes add to the bits (same binade)
+            ab += (uint32_t)(f < nb ? __builtin_amdgcn_readlane(incl - dm, f)
+                                    : __builtin_amdgcn_readlane(incl, 63));
+            PH_MARK(3);
+            EMU_STAT(0, f - from);
 #ifdef LGCN_EMU_STATS
-            if (!fast) {
-                if ((unsigned)(E - 1) >= 254u) EMU_STAT(3, 1);
-                else if ((unsigned)w >= (unsigned)kW) EMU_STAT(4, 1);
-                else if (maxlsb >= E - 127 - 24) EMU_STAT(5, 1);
-                else EMU_STAT(6, 1);
-            }
+            n_fast += f - from;
 #endif
-            LGCN_EMU_FORCE(fast);
-            if (fast) {
-                const int32_t K = __builtin_amdgcn_readlane(cK, idx);
-                ab = neg ? ab - (uint32_t)K : ab + (uint32_t)K;  // same binade: mantissa add
-                EMU_STAT(0, 1);
-                LGCN_EMU_COUNT_FAST();
-                continue;
-            }
-            // re-run block i as the reference does
-            const int64_t bi = er.first_block + b0 + i;
-            const lgcn_emu_block_t bk = blocks[bi];
+            if (f >= nb) break;
+            // re-run block f as the reference does
+            const int32_t kb = b0 + f;
+            const int32_t f_beg = row_beg + kb * LGCN_EMU_BLOCK;
+            const int32_t n = min(f_beg + LGCN_EMU_BLOCK, row_end) - f_beg;
             EMU_STAT(1, 1);
-            EMU_STAT(7, bk.end - bk.beg);
+            EMU_STAT(7, n);
 #ifdef LGCN_EMU_STATS
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            EMU_STAT(2, __builtin_amdgcn_readlane(my_slot, f) < 0);  // not predicted
 #endif
-            SlowData sd;
-            if (pf_block == bi) sd = pf;
-            else slow_load<XD>(sd, edges, bk.beg, bk.end, x, xdiv, x_nz, stage_of(bi), c);
-            if (b0 + i + 1 < er.n_blocks) {
-                const lgcn_emu_block_t nbk = blocks[bi + 1];
-                slow_load<XD>(pf, edges, nbk.beg, nbk.end, x, xdiv, x_nz, stage_of(bi + 1), c);
-                pf_block = bi + 1;
-            }
+            float a;
+            if (stage) {
+                int sl = __builtin_amdgcn_readlane(my_slot, f);
+                if (sl < 0) {  // not predicted: fetch now into the spare slot
+                    sl = NS;
+                    wave_lds_sync();
+                    fetch_slot(kb, sl);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    PH_MARK(5);
+                    PH_COUNT(11, 1);
+                }
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
-            const float a = g_emu_mode == 1 ? __uint_as_float(ab)
-                                            : slow_run(sd, bk.end - bk.beg, stage != nullptr,
-                                                       __uint_as_float(ab), sq);
+                a = g_emu_mode == 1 ? __uint_as_float(ab)
+                                    : slot_chain(n, __uint_as_float(ab), s_v[sl], s_xs[sl]);
 #else
-            const float a = slow_run(sd, bk.end - bk.beg, stage != nullptr, __uint_as_float(ab),
-                                     sq);
+                a = slot_chain(n, __uint_as_float(ab), s_v[sl], s_xs[sl]);
 #endif
+            } else {
+                SlowData sd;
+                slow_load<XD>(sd, edges, f_beg, f_beg + n, x, xdiv, x_nz, nullptr, c);
+                slow_stage(sd, n, false, sq);
+                a = slow_chain(n, __uint_as_float(ab), sq);
+            }
             ab = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(a));
+            PH_MARK(4);
+            PH_COUNT(10, 1);
 #ifdef LGCN_EMU_STATS
             ++n_slow;
             t_slow += __builtin_amdgcn_s_memtime() - t0;
 #endif
+            from = f + 1;
+            if (from >= nb) break;
         }
     }
 #ifdef LGCN_EMU_STATS
+    if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
+        for (int k = 0; k < 16; ++k) g_emu_phase[k] += ph[k];
     if (lane == 0 && blockIdx.x < 256) {
         atomicAdd(&g_emu_row_stats[blockIdx.x][0], n_fast);
         atomicAdd(&g_emu_row_stats[blockIdx.x][1], n_slow);
@@ -625,6 +776,13 @@ int lgcn_emu_stats(unsigned long long* out_host) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 
+
+int lgcn_emu_phase(unsigned long long* out_host) {  // [16], then reset
+    if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_emu_phase), sizeof(g_emu_phase)) != hipSuccess)
+        return -1;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
 
 int lgcn_emu_row_stats(unsigned long long* out_host) {  // [256][4], then reset
     if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_emu_row_stats), sizeof(g_emu_row_stats)) !=

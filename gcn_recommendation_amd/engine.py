@@ -317,7 +317,7 @@ class HubPlan:
                 meta = torch.empty(self.n_emu_blocks * d * LGCN_EMU_META_BYTES, dtype=torch.uint8,
                                    device=device)
                 if emu_stage_enabled():
-                    stage = torch.empty(self.n_emu_blocks * d * LGCN_EMU_BLOCK, **f32)
+                    stage = torch.empty(self.n_emu_blocks * (d + 1) * LGCN_EMU_BLOCK, **f32)
             self._scratch[d] = (part, rel, meta, stage)
         return self._scratch[d]
 
@@ -726,7 +726,7 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
         _check(lib.lgcn_emu_blocks(
             _ptr(graph.edges), plan.emu_blocks + b0 * bb, b1 - b0, x, x_div, _ptr(x_nz), d,
             plan.emu_rel + b0 * d * LGCN_EMU_CANDS * 4, plan.emu_meta + b0 * d * LGCN_EMU_META_BYTES,
-            plan.emu_stage + b0 * d * LGCN_EMU_BLOCK * 4 if plan.emu_stage else None, ss),
+            plan.emu_stage + b0 * (d + 1) * LGCN_EMU_BLOCK * 4 if plan.emu_stage else None, ss),
             "lgcn_emu_blocks")
     rest = PlanT.from_buffer_copy(plan)
     rest.n_emu_rows = rest.n_emu_blocks = 0

@@ -127,8 +127,9 @@ typedef struct {
  *  - emu_*: rows reproduced exactly by block emulation (lgcn_emu_blocks + lgcn_emu_walk);
  *    emu_rel [n_emu_blocks x d x LGCN_EMU_CANDS] 4-byte words and emu_meta [n_emu_blocks x d x
  *    LGCN_EMU_META_BYTES] are caller scratch; emu_stage (optional, NULL = off) [n_emu_blocks x
- *    d x LGCN_EMU_BLOCK] fp32 scratch: the block pass writes each block's X elements per column
- *    there, so a block the walk must re-run reads them contiguously instead of gathering.
+ *    (d + 1) x LGCN_EMU_BLOCK] fp32 scratch: the block pass writes each block's X elements per
+ *    column there (and its edge values as column d), so a block the walk must re-run is read
+ *    contiguously (LDS-DMA) instead of gathered.
  * threshold: rows of degree <= threshold run as bundles in the layer kernel; every row above it
  * must be covered by exactly one of: chunk items, a long-row item, an emulated row. */
 typedef struct {

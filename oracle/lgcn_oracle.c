@@ -37,6 +37,26 @@ void oracle_spmm_coo(int64_t nnz, const int64_t* rows, const int64_t* cols, cons
     }
 }
 
+/* Selected rows of Â·X: y[i,:] = row sel[i] of oracle_spmm_coo's result. A row's value is the
+ * chain over its own nonzeros only, in stored order, so for a row-sorted COO (main.py:331-336
+ * stores one) the chain of row r is nonzeros rowptr[r]..rowptr[r+1]-1 — the same fmaf sequence
+ * oracle_spmm_coo runs for it. Rows are independent: OpenMP over the selection. Used by the
+ * full-size GPU parity tests (BASELINE configs at 56M nonzeros), which check sampled rows of
+ * every layer against this with the GPU's previous layer as X. */
+void oracle_spmm_rows(const int64_t* rowptr, const int64_t* cols, const float* vals, int64_t d,
+                      const float* x, int64_t n_sel, const int64_t* sel, float* y) {
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < n_sel; ++i) {
+        float* yr = y + i * d;
+        for (int64_t c = 0; c < d; ++c) yr[c] = 0.0f;
+        for (int64_t j = rowptr[sel[i]]; j < rowptr[sel[i] + 1]; ++j) {
+            const float v = vals[j];
+            const float* xr = x + cols[j] * d;
+            for (int64_t c = 0; c < d; ++c) yr[c] = fmaf(v, xr[c], yr[c]);
+        }
+    }
+}
+
 /* lightgcn.py:40-54 — final[n x d] = mean(E0..EK). layers_out (optional) receives E1..EK
  * back to back ([K][n][d]). */
 void oracle_forward(int64_t nnz, const int64_t* rows, const int64_t* cols, const float* vals,

@@ -49,8 +49,9 @@ def _load():
     lib.oracle_forward.argtypes = [i64, p, p, p, i64, i64, i64, p, p, p]
     lib.oracle_backward.argtypes = [i64, p, p, p, i64, i64, i64, p, p]
     lib.oracle_forward_f64.argtypes = [i64, p, p, p, i64, i64, i64, p, p]
+    lib.oracle_spmm_rows.argtypes = [p, p, p, i64, p, i64, p, p]
     for f in (lib.oracle_spmm_coo, lib.oracle_forward, lib.oracle_backward,
-              lib.oracle_forward_f64):
+              lib.oracle_forward_f64, lib.oracle_spmm_rows):
         f.restype = None
     _lib = lib
     return lib
@@ -110,6 +111,21 @@ def spmm(rows, cols, vals, n_rows, x):
     y = np.empty((n_rows, x.shape[1]), np.float32)
     _load().oracle_spmm_coo(len(vals), _ptr(rows), _ptr(cols), _ptr(vals), n_rows, x.shape[1],
                             _ptr(x), _ptr(y))
+    return y
+
+
+def spmm_rows(rowptr, cols, vals, x, sel):
+    """Rows `sel` of Â·X for a row-sorted COO given as CSR (rowptr int64 [n+1] over the stored
+    order): each row is the same sequential fmaf chain `spmm` runs for it."""
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    cols = np.ascontiguousarray(cols, dtype=np.int64)
+    vals = np.ascontiguousarray(vals, dtype=np.float32)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    sel = np.ascontiguousarray(sel, dtype=np.int64)
+    assert sel.size == 0 or (sel.min() >= 0 and sel.max() < rowptr.size - 1)
+    y = np.empty((sel.size, x.shape[1]), np.float32)
+    _load().oracle_spmm_rows(_ptr(rowptr), _ptr(cols), _ptr(vals), x.shape[1], _ptr(x), sel.size,
+                             _ptr(sel), _ptr(y))
     return y
 
 

@@ -242,7 +242,7 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
     U, I, B, d, K = case_dims(z)
     n = U + I + B
     thr = engine.INT32_MAX if mode == "chain" else 16
-    kw = dict(mode="chunk" if mode == "chunk" else "exact", emu_min=32)
+    kw = dict(mode="chunk" if mode == "chunk" else "exact", emu_min=48)  # degrees 37..60
     lib = engine.load_library()
     P = engine._ptr
     g = engine.graph_from_coo(_adj(z, gpu_device))
@@ -262,7 +262,7 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
                                     engine.rows_desc(segs, d), d, K,
                                     ctypes.cast(bufs, ctypes.c_void_p), P(out), None, st)
     assert rc == 0
-    want = engine.propagate_forward(g, segs, K, thr, hub_mode=kw["mode"], emu_min=32)
+    want = engine.propagate_forward(g, segs, K, thr, hub_mode=kw["mode"], emu_min=48)
     assert torch.equal(out, want)
     ref = oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], case_e0(z), K)
     if mode != "chunk":
@@ -278,7 +278,7 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
                                      ctypes.byref(plan_t), engine.rows_desc([G], d), None, d, K,
                                      P(work), P(ge0), st)
     assert rc == 0
-    bkw = dict(sparse="off", hub_mode=kw["mode"], emu_min=32)
+    bkw = dict(sparse="off", hub_mode=kw["mode"], emu_min=48)
     assert torch.equal(ge0, engine.propagate_backward(g, [G], K, thr, **bkw))
     if mode != "chunk":
         assert np.array_equal(ge0.cpu().numpy(), oracle.backward(
@@ -375,7 +375,7 @@ def test_row_sparse_backward_bitwise(gpu_device, order, d):
 
 @ORDERS
 def test_hub_rows_chunked_vs_exact(gpu_device, order):
-    """A 20k-edge hub row: chunked (default) within tolerance, exact mode bitwise; both
+    """A 20k-edge hub row: chunked within tolerance, the plain chain and the exact plan bitwise; all
     deterministic run to run."""
     rng = np.random.default_rng(3)
     n, d = 30000, 64
@@ -394,11 +394,15 @@ def test_hub_rows_chunked_vs_exact(gpu_device, order):
     want = oracle.forward(r, c, v, e0, 3)
     exact = engine.propagate_forward(g, x, 3, hub_threshold=engine.INT32_MAX).cpu().numpy()
     assert np.array_equal(exact, want)
-    a = engine.propagate_forward(g, x, 3, hub_threshold=256).cpu().numpy()
-    b = engine.propagate_forward(g, x, 3, hub_threshold=256).cpu().numpy()
+    a = engine.propagate_forward(g, x, 3, hub_threshold=256, hub_mode="chunk").cpu().numpy()
+    b = engine.propagate_forward(g, x, 3, hub_threshold=256, hub_mode="chunk").cpu().numpy()
     assert np.array_equal(a, b)
     assert_close_normwise(a, want, what="chunked hub")
-    assert g.hubs(256).n_rows >= 1
+    assert g.hubs(256, mode="chunk").n_rows >= 1
+    # the default (exact) plan: the hub row emulated in blocks, bitwise
+    ex = engine.propagate_forward(g, x, 3, hub_threshold=256, hub_mode="exact", emu_min=4096)
+    assert g.hubs(256, mode="exact", emu_min=4096).n_emu_rows >= 1
+    assert np.array_equal(ex.cpu().numpy(), want)
 
 
 def expected_slot_order(rp, cols, keyed=True):
@@ -444,7 +448,7 @@ def test_degree_order_plan(gpu_device, monkeypatch, keyed):
         row = ids[s]
         assert np.array_equal(e[rp_s[s]:rp_s[s + 1]], want[rp[row]:rp[row + 1]])
     assert np.array_equal(g.degrees(), deg)
-    hp = g.hubs(16)
+    hp = g.hubs(16, mode="chunk")
     hub_rows = hp.rows.cpu().numpy()[:, 0]
     assert hub_rows.size > 0
     assert np.array_equal(np.sort(hub_rows), np.sort(np.nonzero(deg > 16)[0]))

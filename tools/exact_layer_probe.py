@@ -1,0 +1,109 @@
+"""Component timing of one exact-mode layer on the C3 power-law graph, per emulation threshold:
+the emulation block pass, the layer kernel (bundles + whole long rows), the walk (all rows and
+the longest row alone), each serialised on one stream, then the layer as spmm_layer runs it
+(emulation on side streams beside the layer kernel).
+
+    python tools/exact_layer_probe.py [--emu-min 4096,65536,...] [--layers 2]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from gcn_recommendation_amd import engine  # noqa: E402
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--emu-min", default="4096,32768,131072,524288")
+    ap.add_argument("--layers", type=int, default=2)
+    a = ap.parse_args()
+    cfg = bench.CONFIGS[a.config]
+    dev = torch.device("cuda:0")
+    lib = engine.load_library()
+    r, c, v, _, _, _ = bench.make_graph(cfg, "powerlaw", 16)
+    U, I = cfg["users"], cfg["items"]
+    n, d = U + I, cfg["d"]
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack((r, c))), torch.from_numpy(v),
+                                  (n, n)).to(dev)
+    g = engine.graph_from_coo(adj)
+    gen = torch.Generator().manual_seed(42)
+    e0 = [bench.xavier(U, d, gen).to(dev), bench.xavier(I, d, gen).to(dev)]
+    st = engine._stream(dev)
+    P = engine._ptr
+    ep = engine._epilogue(engine.LGCN_EPI_STORE)
+    y = torch.empty((n, d), device=dev)
+    deg = np.sort(g.degrees())[::-1]
+    chunk_ms = None
+    for emu_min in [int(t) for t in a.emu_min.split(",")]:
+        hp = g.hubs(128, mode="exact", emu_min=emu_min)
+        plan = hp.struct(d, dev)
+        rest = engine.PlanT.from_buffer_copy(plan)
+        rest.n_emu_rows = rest.n_emu_blocks = 0
+        args = (P(g.rowptr), P(g.edges), P(g.row_ids), g.n_rows)
+        print(f"emu_min {emu_min}: long rows {hp.n_long}, emulated rows {hp.n_emu_rows} "
+              f"({hp.n_emu_blocks} blocks, {int(deg[:hp.n_emu_rows].sum()):,} edges)", flush=True)
+        xs = e0
+        for layer in range(1, a.layers + 1):
+            x = engine.rows_desc(xs, d)
+            t = {}
+            t["layer_kernel"] = timed(lambda: lib.lgcn_layer(*args, ctypes.byref(rest), x, 1.0,
+                                                             None, P(y), d, d, ctypes.byref(ep),
+                                                             st))
+            if hp.n_emu_rows:
+                def blocks():
+                    assert lib.lgcn_emu_blocks(P(g.edges), plan.emu_blocks, hp.n_emu_blocks, x,
+                                               1.0, None, d, plan.emu_rel, plan.emu_meta,
+                                               plan.emu_stage, st) == 0
+                t["block_pass"] = timed(blocks)
+
+                def walk(lo, hi):
+                    assert lib.lgcn_emu_walk(P(g.edges), plan.emu_blocks,
+                                             hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
+                                             plan.emu_meta, plan.emu_stage, x, 1.0, None, P(y),
+                                             d, d, ctypes.byref(ep), st) == 0
+                t["walk_all"] = timed(lambda: walk(0, hp.n_emu_rows))
+                t["walk_row0"] = timed(lambda: walk(0, 1))
+                if hp.n_emu_rows > 1:
+                    t["walk_rows_1+"] = timed(lambda: walk(1, hp.n_emu_rows))
+            t["layer_overlapped"] = timed(lambda: engine.spmm_layer(g, xs, y, d, ep, 128, hp))
+            os.environ["LGCN_EMU_OVERLAP"] = "0"
+            t["layer_serial"] = timed(lambda: engine.spmm_layer(g, xs, y, d, ep, 128, hp))
+            del os.environ["LGCN_EMU_OVERLAP"]
+            if chunk_ms is None or layer not in chunk_ms:
+                chunk_ms = chunk_ms or {}
+                hc = g.hubs(128, mode="chunk")
+                chunk_ms[layer] = timed(lambda: engine.spmm_layer(g, xs, y, d, ep, 128, hc))
+            t["chunk_mode_layer"] = chunk_ms[layer]
+            print(f"  layer {layer}: " + ", ".join(f"{k} {val:.3f}" for k, val in t.items()),
+                  flush=True)
+            if layer < a.layers:
+                nxt = torch.empty((n, d), device=dev)
+                engine.spmm_layer(g, xs, nxt, d, ep, 128, hp)
+                xs = [nxt]
+        del plan, rest
+        hp._scratch.clear()
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,19 @@ def stats(lib):
     return dict(zip(NAMES, list(buf)))
 
 
+PHASES = ["stage", "predict", "fetch+wait", "scans", "chains", "on-demand fetch", "-", "-",
+          "chunks", "predicted", "re-run", "not predicted"]
+
+
+def phase_stats(lib):
+    buf = (ctypes.c_ulonglong * 16)()
+    assert lib.lgcn_emu_phase(buf) == 0
+    t = sum(buf[:8])
+    print("  row 0 col 0 walker phases (s_memtime ticks, share): " + ", ".join(
+        f"{n} {buf[k]} ({100 * buf[k] / max(t, 1):.0f}%)" for k, n in enumerate(PHASES[:6])) +
+        "; " + ", ".join(f"{n} {buf[k]}" for k, n in enumerate(PHASES) if k >= 8), flush=True)
+
+
 def row_stats(lib, hp, d, quiet=False):
     buf = (ctypes.c_ulonglong * 1024)()
     assert lib.lgcn_emu_row_stats(buf) == 0
@@ -61,6 +74,7 @@ def main():
         lib.lgcn_emu_stats.argtypes = [ctypes.c_void_p]
         lib.lgcn_emu_row_stats.argtypes = [ctypes.c_void_p]
         lib.lgcn_emu_set_mode.argtypes = [ctypes.c_int]
+        lib.lgcn_emu_phase.argtypes = [ctypes.c_void_p]
     r, c, v, _, _, _ = bench.make_graph(cfg, a.gen, 16)
     U, I, B = cfg["users"], cfg["items"], cfg.get("brands", 0)
     n, d, K = U + I + B, cfg["d"], cfg["K"]
@@ -100,6 +114,7 @@ def per_layer_stats(lib, g, segs, d, K, thr, emu_min, hp):
     n = g.n_rows
     stats(lib)
     row_stats(lib, hp, d, quiet=True)
+    phase_stats(lib)
     layers = [torch.empty((n, d), device=g.device) for _ in range(K)]
     xs = segs
     for k in range(K):
@@ -112,6 +127,7 @@ def per_layer_stats(lib, g, segs, d, K, thr, emu_min, hp):
         r0 = np.array(buf[:4], dtype=np.float64)
         print(f"  layer {k + 1}: all rows {st}; row 0 fast {r0[0] / d:.0f} slow {r0[1] / d:.0f} "
               f"per column", flush=True)
+        phase_stats(lib)
         xs = [layers[k]]
 
 
