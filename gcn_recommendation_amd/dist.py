@@ -576,6 +576,8 @@ def rowpart_secondary(r, c, v, n, nnz, K, d, emb_host, world, rank, args, dev, h
     out = {"ms_per_step": round(ms_max, 3), "edges_per_s": round(K * nnz / (ms_max / 1e3), 1),
            "local_layers_ms": round(local_ms, 3), "exchange_ms": round(ex_ms, 3),
            "received_bytes_per_step_per_rank": int(recv),
+           "padding_ratio": round(world * plan.n_max / n, 4),
+           "exchange_bytes_per_layer_per_rank": int(plan.exchange_bytes_per_layer(d)),
            "exchange_GBps_per_rank": round(recv / (ex_ms / 1e3) / 1e9, 1),
            "what": "rowpart (north_star): row blocks + in-place all_gather_into_tensor of every "
                    "layer's slice (RCCL); exchange = step time - local layer kernels"}

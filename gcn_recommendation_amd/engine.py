@@ -806,25 +806,11 @@ def rows_nonzero(segments, d, device):
     return mask, count
 
 
-def _live_fraction_sample(segments, n, samples=4096):
-    """Fraction of live (nonzero) rows among `samples` evenly spaced rows (one small sync):
-    decides whether the masked backward pays for its mask pass."""
-    idx = np.unique(np.linspace(0, n - 1, min(samples, n)).astype(np.int64))
-    parts, acc = [], 0
-    for t in segments:
-        sel = idx[(idx >= acc) & (idx < acc + t.shape[0])] - acc
-        if sel.size:
-            parts.append(t.index_select(0, torch.from_numpy(sel).to(t.device)))
-        acc += t.shape[0]
-    rows = torch.cat(parts, 0)
-    return float((rows != 0).any(1).float().mean().item())
-
-
 # Row-sparse backward: the upstream gradient of a BPR batch (main.py:496-497 gathers, then
-# IndexBackward scatters into zeros) has a few thousand live rows out of millions. Below this
-# live fraction the backward skips G's zero rows (bitwise-neutral); env LGCN_SPARSE_GRAD = auto
-# (default) | off | on.
-SPARSE_GRAD_MAX_FRAC = 0.25
+# IndexBackward scatters into zeros) has a few thousand live rows out of millions. The backward
+# builds G's row mask on the device (lgcn_rows_nonzero) and skips G's zero rows (bitwise-neutral)
+# — decided without reading anything back, so a training step stays capturable in a HIP graph.
+# env LGCN_SPARSE_GRAD = auto (default: the mask path) | off (dense path) | on (= auto).
 
 
 def _sparse_grad_mode():
@@ -841,8 +827,9 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
     grad_out: the [n x d] upstream gradient, or a list of row blocks (the user / item / brand
     output gradients, read in place). c = G/(K+1) is never materialised: layer 1 divides on
     load and every epilogue adds G[row]/(K+1) — the same rounding as a stored c.
-    sparse: "auto" | "off" | "on" (default: env LGCN_SPARSE_GRAD): with a row-sparse G, layer 1
-    gathers only G's live rows and the epilogues skip its zero rows — same bits, fewer bytes."""
+    sparse: "auto" | "off" | "on" (default: env LGCN_SPARSE_GRAD): auto/on build G's row mask on
+    the device, layer 1 gathers only G's live rows and the epilogues skip its zero rows — same
+    bits, fewer bytes for a BPR batch's G; off runs the dense kernels. Nothing is read back."""
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
     gt = graph.transpose
@@ -863,8 +850,9 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         hp = gt.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         mode = sparse or _sparse_grad_mode()
         nz = None
-        if mode == "on" or (mode == "auto" and n > 0 and
-                            _live_fraction_sample(segs, n) <= SPARSE_GRAD_MAX_FRAC):
+        if mode in ("auto", "on") and n > 0:
+            # no host decision (a read-back would sync every step): the mask costs one pass over
+            # G (0.7 ms at C3) and a dense G runs the masked kernels at the dense rate
             nz, _ = rows_nonzero(segs, d, dev)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
         ep = _epilogue(LGCN_EPI_ADD, addend=g, div=float(K + 1))
