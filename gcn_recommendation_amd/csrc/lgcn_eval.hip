@@ -276,7 +276,7 @@ int lgcn_score_topk(const float* user_emb, int64_t ld_u, const int32_t* users, i
                     int32_t* top_idx, void* stream) {
     if (n_users < 0 || n_items < 0 || k < 1 || k > kCompact || n_splits < 1 || n_splits > 256)
         return LGCN_EINVAL;
-    if (d != 64 && d != 128) return LGCN_EINVAL;
+    if (d != 32 && d != 64 && d != 128 && d != 256) return LGCN_EINVAL;
     if (ld_u % 4 || ld_i % 4 || (reinterpret_cast<uintptr_t>(user_emb) & 15) ||
         (reinterpret_cast<uintptr_t>(item_emb) & 15))
         return LGCN_EALIGN;
@@ -290,21 +290,26 @@ int lgcn_score_topk(const float* user_emb, int64_t ld_u, const int32_t* users, i
     if (split_len == 0) split_len = 32;
     const dim3 grid((n_users + kWaves * kUsersPerWave - 1) / (kWaves * kUsersPerWave), n_splits);
     const size_t lds = sizeof(WaveState) * kWaves;
+    const void* fn = d == 32    ? reinterpret_cast<const void*>(k_score_topk<32>)
+                     : d == 64  ? reinterpret_cast<const void*>(k_score_topk<64>)
+                     : d == 128 ? reinterpret_cast<const void*>(k_score_topk<128>)
+                                : reinterpret_cast<const void*>(k_score_topk<256>);
     {
-        const hipError_t ea = hipFuncSetAttribute(
-            d == 64 ? reinterpret_cast<const void*>(k_score_topk<64>)
-                    : reinterpret_cast<const void*>(k_score_topk<128>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const hipError_t ea =
+            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ea != hipSuccess) return (int)ea;
     }
-    if (d == 64)
-        hipLaunchKernelGGL(k_score_topk<64>, grid, dim3(kWaves * 64), lds, s, user_emb, ld_u, users,
-                           n_users, item_emb, ld_i, n_items, split_len, mask_rowptr, mask_items, k,
-                           part_scores, part_idx);
-    else
-        hipLaunchKernelGGL(k_score_topk<128>, grid, dim3(kWaves * 64), lds, s, user_emb, ld_u,
-                           users, n_users, item_emb, ld_i, n_items, split_len, mask_rowptr,
-                           mask_items, k, part_scores, part_idx);
+#define LGCN_SCORE_LAUNCH(D_)                                                                   \
+    hipLaunchKernelGGL(k_score_topk<D_>, grid, dim3(kWaves * 64), lds, s, user_emb, ld_u, users, \
+                       n_users, item_emb, ld_i, n_items, split_len, mask_rowptr, mask_items, k,  \
+                       part_scores, part_idx)
+    switch (d) {
+        case 32: LGCN_SCORE_LAUNCH(32); break;
+        case 64: LGCN_SCORE_LAUNCH(64); break;
+        case 128: LGCN_SCORE_LAUNCH(128); break;
+        default: LGCN_SCORE_LAUNCH(256); break;
+    }
+#undef LGCN_SCORE_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     const size_t mlds = (size_t)n_splits * k * 8;

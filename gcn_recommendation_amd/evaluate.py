@@ -91,7 +91,7 @@ def topk_fused(user_emb, item_emb, users, mask_rowptr, mask_items, k=20):
     return top_s[:n], top_i[:n]
 
 
-FUSED_DIMS = (64, 128)   # lgcn_score_topk's widths (include/lgcn.h)
+FUSED_DIMS = (32, 64, 128, 256)   # lgcn_score_topk's widths (include/lgcn.h)
 FUSED_MAX_K = 32
 
 

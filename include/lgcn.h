@@ -364,7 +364,7 @@ int lgcn_eval_splits(int32_t n_users, int32_t n_items, int32_t n_cu);
  * [n_users x n_items] score matrix: scores = user_emb[users[b]] · item_emb[i] (exact-f32 MFMA,
  * an ordered fmaf chain), items of user u listed in mask_items[mask_rowptr[u]:mask_rowptr[u+1]]
  * (sorted ascending) score -1e10, ties broken by lower item index. Outputs top_scores/top_idx
- * [n_users x k] in rank order (-inf / -1 past n_items). d in {64, 128}, k in [1, 32], 16-B
+ * [n_users x k] in rank order (-inf / -1 past n_items). d in {32, 64, 128, 256}, k in [1, 32], 16-B
  * aligned rows. part_scores/part_idx: scratch [n_splits x n_users x k]. */
 int lgcn_score_topk(const float* user_emb, int64_t ld_u, const int32_t* users, int32_t n_users,
                     const float* item_emb, int64_t ld_i, int32_t n_items, int32_t d,

@@ -24,7 +24,8 @@ from conftest import ROOT
 from gcn_recommendation_amd import engine
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+# full-size graphs: the host generator + CSR plan take ~1 min per graph on the box
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402  (the bench's synthetic Books-shape generator)

@@ -600,13 +600,13 @@ def test_device_adjacency_builder_c2_powerlaw(gpu_device):
 @pytest.mark.parametrize("name", CASES)
 def test_fused_evaluate_matches_reference(gpu_device, name):
     """evaluate.evaluate reproduces the reference's evaluate numbers (main.py:404-439) on the
-    golden cases: on the fused score+mask+topk kernel for d in {64, 128}, on torch ops for the
-    other widths (d = 12, 32 here) — the reference takes any d and k, so does the drop-in."""
+    golden cases: on the fused score+mask+topk kernel for d in {32, 64, 128, 256}, on torch ops
+    for the other widths (d = 12 here) — the reference takes any d and k, so does the drop-in."""
     import pandas as pd
     from gcn_recommendation_amd import evaluate as E
     z = load_case(name)
     U, I, B, d, K = case_dims(z)
-    assert E.fused_supported(d, int(z["eval_k"])) == (d in (64, 128))
+    assert E.fused_supported(d, int(z["eval_k"])) == (d in (32, 64, 128, 256))
     m = _model(z, gpu_device)
     va = pd.DataFrame({"user_idx": z["val_user"], "item_idx": z["val_item"]})
     tr = pd.DataFrame({"user_idx": z["train_user"], "item_idx": z["train_item"]})
@@ -615,7 +615,7 @@ def test_fused_evaluate_matches_reference(gpu_device, name):
     assert abs(ndcg - float(z["ndcg"])) < 1e-12
 
 
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
 def test_fused_topk_vs_torch(gpu_device, d):
     """lgcn_score_topk vs matmul + mask + torch.topk on 3000 users x 70k items: identical lists
     except where two scores are within fp32 rounding of each other (different summation order)."""

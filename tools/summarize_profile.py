@@ -49,7 +49,10 @@ def main(prof, tag, rnd, algo_bytes):
     store = [k for k in kernels if "k_layer" in k and layer_mode(k) == 0]
     store = store or [k for k in kernels if "k_layer" in k]
     dom = max(store, key=lambda k: (kernels[k]["avg_ms"] or 0) * (kernels[k]["calls"] or 0))
+    sys.path.insert(0, ROOT)
+    from bench import kernel_source_hash  # bench.py refuses a traffic file with another stamp
     out = {"command": f"tools/profile.sh {tag} ... (see profiles/README.md)",
+           "source_hash": kernel_source_hash(),
            "correction": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE "
                          "halves 16-B/lane coalesced reads)",
            "kernel": dom, "avg_duration_ms_rocprof": kernels[dom]["avg_ms"],
