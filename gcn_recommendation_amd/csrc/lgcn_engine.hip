@@ -653,7 +653,7 @@ static int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int
     if (int e = hub_combine(p.rows, p.n_rows, p.n_pre, p.partials, y, ldy, d, ep, s)) return e;
     if (p.n_emu_rows > 0) {
         if (int e = lgcn_emu_walk(edges, p.emu_blocks, p.emu_rows, p.n_emu_rows, p.emu_rel,
-                                  p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, s))
+                                  p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, 0, s))
             return e;
     }
     return 0;

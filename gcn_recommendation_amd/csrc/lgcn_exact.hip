@@ -414,7 +414,7 @@ __device__ unsigned long long g_emu_phase[16];
 // once.
 // A block that fails without having been predicted is fetched on demand into a spare slot.
 #define LGCN_EMU_CH 64
-#define LGCN_EMU_SLOTS 15   // predicted re-run blocks per chunk with LDS slots (+1 spare)
+#define LGCN_EMU_SLOTS 15   // default predicted re-run blocks per chunk with LDS slots (+1 spare)
 
 struct EmuChunk {  // one lane's share of a chunk's raw records
     int32_t lo, hi, pk;                 // meta of block `lane`
@@ -496,15 +496,17 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                                                  const float* __restrict__ stage, lgcn_rows_t x,
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
-                                                 lgcn_epilogue_t ep) {
+                                                 lgcn_epilogue_t ep, int NS) {
     constexpr int CH = LGCN_EMU_CH;
     constexpr int NC = LGCN_EMU_CANDS;
-    constexpr int NS = LGCN_EMU_SLOTS;
     static_assert(CH == 64, "one lane per block of a chunk");
     __shared__ int32_t s_k[CH * NC], s_min[CH * NC], s_max[CH * NC];
-    __shared__ float s_v[NS + 1][LGCN_EMU_BLOCK];    // re-run blocks' edge values
-    __shared__ float s_xs[NS + 1][LGCN_EMU_BLOCK];   // ... and their X elements
     __shared__ float2 sq[LGCN_EMU_BLOCK];            // no-stage mode: gathered (val, x)
+    // NS + 1 slots (dynamic LDS, sized at launch): re-run blocks' edge values, then their X
+    // elements. Fewer slots = less LDS per wave = more walk waves per CU (short-row parts).
+    extern __shared__ __attribute__((aligned(16))) float s_dyn[];
+    auto s_v = [&](int sl) { return s_dyn + sl * LGCN_EMU_BLOCK; };
+    auto s_xs = [&](int sl) { return s_dyn + (NS + 1 + sl) * LGCN_EMU_BLOCK; };
     const int lane = threadIdx.x;
     const int c = blockIdx.y;
     const lgcn_emu_row_t er = rows[blockIdx.x];
@@ -553,8 +555,8 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     const int32_t row_end = blocks[er.first_block + er.n_blocks - 1].end;
     auto fetch_slot = [&](int32_t kb, int s) {
         const int64_t bi = er.first_block + kb;
-        fetch_block_lds(stage + (bi * (d + 1) + d) * LGCN_EMU_BLOCK, stage_of(bi), s_v[s],
-                        s_xs[s]);
+        fetch_block_lds(stage + (bi * (d + 1) + d) * LGCN_EMU_BLOCK, stage_of(bi), s_v(s),
+                        s_xs(s));
     };
 #ifdef LGCN_EMU_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
@@ -662,9 +664,9 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                 }
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
                 a = g_emu_mode == 1 ? __uint_as_float(ab)
-                                    : slot_chain(n, __uint_as_float(ab), s_v[sl], s_xs[sl]);
+                                    : slot_chain(n, __uint_as_float(ab), s_v(sl), s_xs(sl));
 #else
-                a = slot_chain(n, __uint_as_float(ab), s_v[sl], s_xs[sl]);
+                a = slot_chain(n, __uint_as_float(ab), s_v(sl), s_xs(sl));
 #endif
             } else {
                 SlowData sd;
@@ -732,10 +734,11 @@ template <int MODE, int XD>
 int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                 const lgcn_emu_row_t* rows, int32_t n_rows, const int32_t* rel, const EmuMeta* meta,
                 const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
-                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
     const dim3 grid((uint32_t)n_rows, (uint32_t)d);
-    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), 0, s, edges, blocks, rows, rel, meta,
-                       stage, x, xdiv, x_nz, d, y, ldy, ep);
+    const size_t lds = (size_t)2 * (slots + 1) * LGCN_EMU_BLOCK * sizeof(float);
+    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, rel,
+                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots);
     return herr_x(hipGetLastError());
 }
 
@@ -747,9 +750,9 @@ template <int MODE>
 int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
               const lgcn_emu_row_t* rows, int32_t n_rows, const int32_t* rel, const EmuMeta* meta,
               const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
-              int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+              int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
 #define LGCN_W(XD_) \
-    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, rel, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, s);
+    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, rel, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, s);
     switch (xd) {
         LGCN_W(0) LGCN_W(1) LGCN_W(2) LGCN_W(4) LGCN_W(5) LGCN_W(6)
         default: return LGCN_EINVAL;
@@ -816,8 +819,12 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
 int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
-                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* stream) {
-    if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host) return LGCN_EINVAL;
+                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
+                  void* stream) {
+    if (slots == 0) slots = LGCN_EMU_SLOTS;
+    if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host || slots < 1 ||
+        slots > 63)
+        return LGCN_EINVAL;
     if (n_rows == 0) return 0;
     if (!edges || !blocks || !rows || !rel || !meta || !y || ldy < d || !x.p0) return LGCN_EINVAL;
     lgcn_epilogue_t ep = *epi_host;
@@ -839,11 +846,11 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     const int32_t* rl = reinterpret_cast<const int32_t*>(rel);
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, s);
+            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         case LGCN_EPI_MEAN:
-            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, s);
+            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         case LGCN_EPI_ADD:
-            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, s);
+            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         default:
             return LGCN_EINVAL;
     }

@@ -24,7 +24,7 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
-ABI_VERSION = 5
+ABI_VERSION = 6
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 32, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -138,7 +138,7 @@ ABI = [
     ("lgcn_emu_blocks", ctypes.c_int, [_P, _P, _I32, RowsT, ctypes.c_float, _P, _I32, _P, _P, _P,
                                        _P]),
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
-                                     _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
+                                     _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P]),
     ("lgcn_layer", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, ctypes.c_float, _P,
                                   _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _I32,
@@ -670,11 +670,22 @@ _side_streams = {}
 
 
 def _side_stream(device, i=0):
-    """Per-device side streams the emulated hub rows run on, beside the layer kernel."""
+    """Per-device side streams the emulated hub rows run on, beside the layer kernel. Stream 0
+    carries the longest rows (the layer's critical path): it is created at high priority
+    (LGCN_EMU_PRIORITY=0: normal) so its waves are dispatched ahead of the layer kernel's."""
     key = (str(device), i)
     if key not in _side_streams:
-        _side_streams[key] = torch.cuda.Stream(device)
+        hi = i == 0 and os.environ.get("LGCN_EMU_PRIORITY", "1") != "0"
+        _side_streams[key] = torch.cuda.Stream(device, priority=-1 if hi else 0)
     return _side_streams[key]
+
+
+def emu_slots():
+    """LDS re-run slots of the walk per emulated-row part (longest rows first): env
+    LGCN_EMU_SLOTS="a,b,c" (default 15,15,3 — short rows re-run few blocks per chunk, and fewer
+    slots fit more walk waves per CU)."""
+    v = [int(t) for t in os.environ.get("LGCN_EMU_SLOTS", "15,15,3").split(",") if t.strip()]
+    return v or [0]
 
 
 def emu_overlap_enabled():
@@ -736,12 +747,14 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
                           d, ctypes.byref(epi), stream), "lgcn_layer")
     if kernel_events is not None:
         kernel_events[1].record()
-    for sd, (r0, r1, b0, b1) in zip(sides, parts):
+    slots = emu_slots()
+    for i, (sd, (r0, r1, b0, b1)) in enumerate(zip(sides, parts)):
         if r1 <= r0:
             continue
         _check(lib.lgcn_emu_walk(_ptr(graph.edges), plan.emu_blocks, plan.emu_rows + r0 * rb,
                                  r1 - r0, plan.emu_rel, plan.emu_meta, plan.emu_stage, x, x_div,
                                  _ptr(x_nz), _ptr(y), y.stride(0), d, ctypes.byref(epi),
+                                 slots[min(i, len(slots) - 1)],
                                  ctypes.c_void_p(sd.cuda_stream)), "lgcn_emu_walk")
     for sd in sides:
         main.wait_stream(sd)        # every row of Y written

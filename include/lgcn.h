@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 5
+#define LGCN_ABI_VERSION 6
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -299,11 +299,14 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
 
 /* Emulation walk: each emulated row's final value per column (bitwise the sequential chain),
  * epilogue applied, written to Y. Needs lgcn_emu_blocks' rel / meta (and stage, if it wrote
- * one; NULL = re-run blocks gather X) of the same X. */
+ * one; NULL = re-run blocks gather X) of the same X. slots: LDS slots for predicted re-run
+ * blocks per 64-block chunk, 1..63 (0 = LGCN_EMU_SLOTS): 2 KB of LDS per wave each, so a walk
+ * over short rows (few re-runs per chunk) runs more waves per CU with fewer slots. */
 int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
-                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* stream);
+                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
+                  void* stream);
 
 /* One whole layer under a hub plan: emulation block pass, lgcn_spmm_layer (bundles, chunks and
  * long rows), chunk combine, emulation walk — every row of Y written once. */

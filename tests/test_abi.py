@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 5
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 6
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -82,7 +82,9 @@ def test_argument_validation_without_gpu(lib):
     assert lib.lgcn_emu_blocks(None, None, -1, rows, 1.0, None, 64, None, None, None, None) == -1
     assert lib.lgcn_emu_blocks(None, None, 0, rows, 1.0, None, 64, None, None, None, None) == 0
     assert lib.lgcn_emu_walk(None, None, None, 2, None, None, None, rows, 1.0, None, None, 64, 64,
-                             ctypes.byref(ep), None) == -1
+                             ctypes.byref(ep), 0, None) == -1
+    assert lib.lgcn_emu_walk(None, None, None, 0, None, None, None, rows, 1.0, None, None, 64, 64,
+                             ctypes.byref(ep), 64, None) == -1   # slots out of range
     assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 0
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,

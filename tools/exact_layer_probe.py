@@ -80,7 +80,7 @@ def main():
                     assert lib.lgcn_emu_walk(P(g.edges), plan.emu_blocks,
                                              hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
                                              plan.emu_meta, plan.emu_stage, x, 1.0, None, P(y),
-                                             d, d, ctypes.byref(ep), st) == 0
+                                             d, d, ctypes.byref(ep), 0, st) == 0
                 t["walk_all"] = timed(lambda: walk(0, hp.n_emu_rows))
                 t["walk_row0"] = timed(lambda: walk(0, 1))
                 if hp.n_emu_rows > 1:
