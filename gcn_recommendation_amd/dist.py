@@ -250,10 +250,10 @@ class FeatSplitPlan:
         e0 = torch.cat([t[:, c0:c1] for t in segments], 0).to(self.device)
         return e0[self.perm].contiguous(), (c0, c1)
 
-    def forward(self, x_slot, K, hub_thr=None, layer_events=None):
+    def forward(self, x_slot, K, hub_thr=None, layer_events=None, hub_mode=None):
         """mean(E0..EK) of this rank's columns, in slot order. No exchange."""
         return engine.propagate_forward(self.graph, [x_slot], K, hub_thr,
-                                        layer_events=layer_events)
+                                        layer_events=layer_events, hub_mode=hub_mode)
 
     def attach_transpose(self, rowptr, cols, vals):
         """Âᵀ in the same slot space, for the backward of a shard (dE0 = Σ_k (Âᵀ)^k G/(K+1)):
@@ -520,7 +520,21 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
                      dtype=torch.float64, device=dev)
     ms_max, kern_ms, all_ms = _max_over_ranks(t)
-    c4 = rp = bwd = None
+    c4 = rp = bwd = chunk = None
+    hub_mode = engine.hub_mode_from_env()
+    if mode == "featsplit" and hub_mode == "exact":
+        # secondary: the same shard forward with chunked hub rows (fixed-order partial sums, not
+        # the reference's rounding on hub rows): the throughput the split gets when the
+        # sequential hub chains (whose walk does not shrink with P) are not reproduced
+        def fn_c(timed):
+            ev = mk_events() if timed else None
+            plan.forward(x_slot, K, hub_thr, layer_events=ev, hub_mode="chunk")
+            return ev
+        ms_c, _ = _timed(fn_c, args.steps, args.warmup, dev)
+        (ms_c,) = _max_over_ranks(torch.tensor([ms_c], dtype=torch.float64, device=dev))
+        chunk = {"ms_per_step": round(ms_c / args.steps, 4),
+                 "edges_per_s": round(K * nnz * args.steps / (ms_c / 1e3), 1),
+                 "what": "hub_mode=chunk on the same shards (not bitwise on hub rows)"}
     if mode == "featsplit" and getattr(args, "backward", True):
         bwd = featsplit_backward_timing(plan, rowptr, c, v, x_slot, K, args, dev, hub_thr)
     if mode == "featsplit" and getattr(args, "c4", True):
@@ -539,14 +553,18 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
         "data": "synthetic",
         "config": {"workload": cfg["name"], "generator": args.gen, "users": U, "items": I,
                    "interactions": cfg["interactions"], "nnz": nnz, "d": d, "layers": K,
-                   "hub_threshold": hub_thr, "parallelism": f"{mode}{world}",
+                   "hub_threshold": hub_thr, "hub_mode": hub_mode,
+                   "parallelism": f"{mode}{world}",
                    "exchange_bytes_per_step_per_rank": int(comm), **extra},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
-                     "unit": "GB/s", "frac": round(achieved / 8000.0, 4),
-                     "traffic": profiled_traffic(cfg, args, mode, d // world if mode == "featsplit"
-                                                 else None),
+                     "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "basis": "algorithmic bytes (SURVEY 8d) / whole-layer time (store layers), "
+                              "per GPU, max over ranks; no PMC pass of this build at N > 1",
+                     "round1_pmc_traffic_chunk_mode": profiled_traffic(
+                         cfg, args, mode, d // world if mode == "featsplit" else None),
                      "kernel": "k_layer store layers, per GPU (max over ranks)",
                      "bytes_per_launch": int(b_layer), "avg_launch_ms": round(kern_ms, 4)},
+        **({"chunk_mode": chunk} if chunk else {}),
         **({"backward": bwd} if bwd else {}),
         **({"c4_same_graph": c4} if c4 else {}),
         **({"rowpart": rp} if rp else {}),

@@ -680,6 +680,9 @@ def _side_stream(device, i=0):
     return _side_streams[key]
 
 
+emu_trace = None  # a list: spmm_layer records (name, event) pairs of its streams' phases into it
+
+
 def emu_slots():
     """LDS re-run slots of the walk per emulated-row part (longest rows first): env
     LGCN_EMU_SLOTS="a,b,c" (default 15,15,3 — short rows re-run few blocks per chunk, and fewer
@@ -726,6 +729,10 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     # rows follow on further side streams (rows are stored longest first)
     parts = hp.emu_parts()
     sides = [_side_stream(graph.device, i) for i in range(len(parts))]
+    tr = emu_trace
+    if tr is not None:  # diagnostics (tools/exact_layer_probe.py): per-stream phase events
+        tr.clear()
+        tr.append(("start", main.record_event(torch.cuda.Event(enable_timing=True))))
     for sd in sides:
         sd.wait_stream(main)        # X (and the epilogue operands) are ready
     rb, bb = hp.emu_rows.element_size() * 4, hp.emu_blocks.element_size() * 4
@@ -739,6 +746,9 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
             plan.emu_rel + b0 * d * LGCN_EMU_CANDS * 4, plan.emu_meta + b0 * d * LGCN_EMU_META_BYTES,
             plan.emu_stage + b0 * (d + 1) * LGCN_EMU_BLOCK * 4 if plan.emu_stage else None, ss),
             "lgcn_emu_blocks")
+        if tr is not None:
+            tr.append((f"part{len(tr) - 1}_blocks", sd.record_event(
+                torch.cuda.Event(enable_timing=True))))
     rest = PlanT.from_buffer_copy(plan)
     rest.n_emu_rows = rest.n_emu_blocks = 0
     if kernel_events is not None:
@@ -747,6 +757,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
                           d, ctypes.byref(epi), stream), "lgcn_layer")
     if kernel_events is not None:
         kernel_events[1].record()
+    if tr is not None:
+        tr.append(("layer_kernel", main.record_event(torch.cuda.Event(enable_timing=True))))
     slots = emu_slots()
     for i, (sd, (r0, r1, b0, b1)) in enumerate(zip(sides, parts)):
         if r1 <= r0:
@@ -756,6 +768,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
                                  _ptr(x_nz), _ptr(y), y.stride(0), d, ctypes.byref(epi),
                                  slots[min(i, len(slots) - 1)],
                                  ctypes.c_void_p(sd.cuda_stream)), "lgcn_emu_walk")
+        if tr is not None:
+            tr.append((f"part{i}_walk", sd.record_event(torch.cuda.Event(enable_timing=True))))
     for sd in sides:
         main.wait_stream(sd)        # every row of Y written
     return y

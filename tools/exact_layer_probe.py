@@ -94,6 +94,13 @@ def main():
                 hc = g.hubs(128, mode="chunk")
                 chunk_ms[layer] = timed(lambda: engine.spmm_layer(g, xs, y, d, ep, 128, hc))
             t["chunk_mode_layer"] = chunk_ms[layer]
+            engine.emu_trace = []
+            engine.spmm_layer(g, xs, y, d, ep, 128, hp)
+            torch.cuda.synchronize()
+            ev0 = engine.emu_trace[0][1]
+            print(f"  layer {layer} phases (ms from start): " + ", ".join(
+                f"{nm} {ev0.elapsed_time(e):.3f}" for nm, e in engine.emu_trace[1:]), flush=True)
+            engine.emu_trace = None
             print(f"  layer {layer}: " + ", ".join(f"{k} {val:.3f}" for k, val in t.items()),
                   flush=True)
             if layer < a.layers:
