@@ -760,6 +760,202 @@ int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
 #undef LGCN_W
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// mid-size hub rows: the reference's sequential chain itself, latency-hidden
+// ---------------------------------------------------------------------------------------------
+// For a row of a few thousand to ~10^5 edges the chain itself is cheap (deg dependent FMAs); what
+// makes it slow in the layer kernel is the gathers. One wave per (row, W-column slice): the
+// wave keeps two 64-edge windows of gathered X rows in flight by LDS-DMA (global_load_lds
+// dwordx4: no registers held, up to 2 * W/4 + 1 loads outstanding) while it folds the window
+// before them, lane c = column c, acc = fma(val_j, x_j, acc) in stored order from +0 — the
+// reference's arithmetic, no emulation, no block pass. Edge records come in by LDS-DMA one
+// window further ahead, so the gather addresses are read from LDS, never waited on alone.
+// Ring: X windows w (folding), w+1 (in flight), w+2 (being issued); records w .. w+3.
+template <int W>
+struct ChainCfg {
+    static constexpr int LPR = W / 4;       // lanes per gathered row slice (16 B each)
+    static constexpr int RPI = 64 / LPR;    // rows per 1-KB LDS-DMA instruction
+    static constexpr int NI = 64 / RPI;     // instructions per 64-edge window
+    static constexpr int XWIN = 64 * W;     // floats per X window
+    static constexpr int NX = 4;            // X windows in the ring (3 in flight while folding)
+    static constexpr int NR = 7;            // record windows in the ring
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+
+// 16 LDS reads at a + OFF + t * STRIDE, completed before the values are used. Inline asm on
+// purpose: LDS written by LDS-DMA makes the compiler wait for EVERY outstanding global load
+// before any compiler-visible LDS read (it cannot tell the ring slots apart), which would drain
+// the gathers in flight; here the waits are explicit (vmcnt before, lgkmcnt inside).
+template <int OFF, int STRIDE>
+__device__ __forceinline__ void lds_read16(uint32_t a, float (&v)[16]) {
+    asm volatile(
+        "ds_read_b32 %0, %16 offset:%17\n\tds_read_b32 %1, %16 offset:%18\n\t"
+        "ds_read_b32 %2, %16 offset:%19\n\tds_read_b32 %3, %16 offset:%20\n\t"
+        "ds_read_b32 %4, %16 offset:%21\n\tds_read_b32 %5, %16 offset:%22\n\t"
+        "ds_read_b32 %6, %16 offset:%23\n\tds_read_b32 %7, %16 offset:%24\n\t"
+        "ds_read_b32 %8, %16 offset:%25\n\tds_read_b32 %9, %16 offset:%26\n\t"
+        "ds_read_b32 %10, %16 offset:%27\n\tds_read_b32 %11, %16 offset:%28\n\t"
+        "ds_read_b32 %12, %16 offset:%29\n\tds_read_b32 %13, %16 offset:%30\n\t"
+        "ds_read_b32 %14, %16 offset:%31\n\tds_read_b32 %15, %16 offset:%32\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+          "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
+          "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
+        : "v"(a), "n"(OFF), "n"(OFF + STRIDE), "n"(OFF + 2 * STRIDE), "n"(OFF + 3 * STRIDE),
+          "n"(OFF + 4 * STRIDE), "n"(OFF + 5 * STRIDE), "n"(OFF + 6 * STRIDE),
+          "n"(OFF + 7 * STRIDE), "n"(OFF + 8 * STRIDE), "n"(OFF + 9 * STRIDE),
+          "n"(OFF + 10 * STRIDE), "n"(OFF + 11 * STRIDE), "n"(OFF + 12 * STRIDE),
+          "n"(OFF + 13 * STRIDE), "n"(OFF + 14 * STRIDE), "n"(OFF + 15 * STRIDE)
+        : "memory");
+}
+
+__device__ __forceinline__ float lds_read1(uint32_t a) {
+    float v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MODE, int XD, int W>
+__global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict__ edges,
+                                                   const lgcn_emu_block_t* __restrict__ blocks,
+                                                   const lgcn_emu_row_t* __restrict__ rows,
+                                                   lgcn_rows_t x, float xdiv, int32_t d,
+                                                   float* __restrict__ y, int64_t ldy,
+                                                   lgcn_epilogue_t ep) {
+    using C = ChainCfg<W>;
+    constexpr int NX = C::NX, NR = C::NR, AHEAD = NX - 1;  // X windows in flight
+    __shared__ __attribute__((aligned(16))) float s_x[NX][C::XWIN];
+    __shared__ __attribute__((aligned(16))) int2 s_rec[NR][64];
+    const int lane = threadIdx.x;
+    const int c0 = blockIdx.y * W;
+    const lgcn_emu_row_t er = rows[blockIdx.x];
+    const int32_t beg = blocks[er.first_block].beg;
+    const int32_t end = blocks[er.first_block + er.n_blocks - 1].end;
+    const int32_t nwin = (end - beg + 63) >> 6;
+    // records of window w -> s_rec[w % NR]: 128 dwords in two dword LDS-DMA loads. Dwords past
+    // the row repeat its last record (col and val kept apart by parity), so windows past the
+    // end load valid records and gather valid rows: every iteration issues the same number of
+    // loads, which keeps the vmcnt arithmetic below exact. They are never folded.
+    const int32_t* ew = reinterpret_cast<const int32_t*>(edges);
+    const int64_t dl = 2 * (int64_t)end - 1, dlast = 2 * (int64_t)end - 2 + (lane & 1);
+    auto rec_dma = [&](int32_t w) {
+        const int64_t d0 = 2 * ((int64_t)beg + 64 * w) + lane;
+        int32_t* dst = reinterpret_cast<int32_t*>(&s_rec[w % NR][0]);
+        __builtin_amdgcn_global_load_lds(ew + (d0 <= dl ? d0 : dlast), dst, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(ew + (d0 + 64 <= dl ? d0 + 64 : dlast), dst + 64, 4, 0, 0);
+    };
+    // gathered X of window w -> s_x[w % NX]: instruction k moves rows k*RPI .. k*RPI + RPI - 1
+    // (lane -> row sub = lane / LPR, 16-B piece q = lane % LPR); the columns come from LDS
+    const int sub = lane / C::LPR, q = lane % C::LPR;
+    auto x_dma = [&](int32_t w) {
+        float cols[16];
+        lds_read16<0, C::RPI * 8>(lds_addr(&s_rec[w % NR][sub]), cols);
+        float* dst = s_x[w % NX];
+#pragma unroll
+        for (int k = 0; k < C::NI; ++k) {
+            const float* src = seg_row_sel(x, __float_as_int(cols[k])) + c0 + 4 * q;
+            __builtin_amdgcn_global_load_lds(src, dst + k * 256, 16, 0, 0);
+        }
+    };
+    // Pipeline (A = AHEAD): iteration v issues x(v + A) then rec(v + 2A); the prologue runs
+    // v = -A .. -1 after rec(0 .. A-1) have landed. At iteration w, x(w) and rec(w + A) (both
+    // issued by iteration w - A) must have landed: A - 1 later iterations of NI + 2 loads each
+    // may still be in flight. Ring slots: x(w + A) reuses window w - 1's slot (NX = A + 1),
+    // rec(w + 2A) record window w - 1's (NR = 2A + 1).
+    static_assert(NX == AHEAD + 1 && NR == 2 * AHEAD + 1, "ring sizes");
+    for (int w = 0; w < AHEAD; ++w) rec_dma(w);
+    wait_vm<0>();
+    for (int v = -AHEAD; v < 0; ++v) {
+        x_dma(v + AHEAD);
+        rec_dma(v + 2 * AHEAD);
+    }
+    float acc = 0.f;
+    const int cc = lane < W ? lane : 0;
+    for (int32_t w = 0; w < nwin; ++w) {
+        wait_vm<(AHEAD - 1) * (C::NI + 2)>();
+        x_dma(w + AHEAD);
+        rec_dma(w + 2 * AHEAD);
+        const int n = min(64, end - beg - 64 * w);
+        const uint32_t xa = lds_addr(&s_x[w % NX][cc]);
+        const float vme = lds_read1(lds_addr(&s_rec[w % NR][lane].y));  // lane j: val of edge j
+#define LGCN_CHAIN_FOLD(G)                                                                    \
+        {                                                                                     \
+            float xv[16];                                                                     \
+            lds_read16<(G) * W * 4, W * 4>(xa, xv);                                           \
+            _Pragma("unroll") for (int t = 0; t < 16; ++t) {                                  \
+                float xe = xv[t];                                                             \
+                if constexpr ((XD & 3) == 1) xe = xe / xdiv;                                  \
+                else if constexpr ((XD & 3) == 2) xe = xe * xdiv;                             \
+                const float v = __int_as_float(                                               \
+                    __builtin_amdgcn_readlane(__float_as_int(vme), (G) + t));                 \
+                acc = (G) + t < n ? __builtin_fmaf(v, xe, acc) : acc;                         \
+            }                                                                                 \
+        }
+        LGCN_CHAIN_FOLD(0)
+        LGCN_CHAIN_FOLD(16)
+        LGCN_CHAIN_FOLD(32)
+        LGCN_CHAIN_FOLD(48)
+#undef LGCN_CHAIN_FOLD
+    }
+    wait_vm<0>();  // no LDS-DMA may land after the wave (and its LDS) is gone
+    if (lane >= W || c0 + lane >= d) return;
+    const int c = c0 + lane;
+    const int32_t row = er.row;
+    float out = acc;
+    if constexpr (MODE == LGCN_EPI_MEAN) {
+        float s = seg_row_x(ep.prev0, row)[c];
+        for (int i = 0; i + 1 < ep.n_prev; ++i) s = s + ep.prev_dense[i][(int64_t)row * ep.ld_prev + c];
+        s = s + out;
+        out = ep.pad ? s * __int_as_float(ep.pad) : s / ep.div;
+    } else if constexpr (MODE == LGCN_EPI_ADD) {
+        if (!ep.addend_nz || row_live_x(ep.addend_nz, row)) {
+            const float z = seg_row_x(ep.addend, row)[c];
+            out = (ep.pad ? z * __int_as_float(ep.pad) : z / ep.div) + out;
+        }
+    }
+    y[(int64_t)row * ldy + c] = out;
+}
+
+template <int MODE, int XD>
+int launch_chain(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                 const lgcn_emu_row_t* rows, int32_t n_rows, const lgcn_rows_t& x, float xdiv,
+                 float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+    const int w = d % 64 == 0 ? 64 : d;  // 16, 32 or a multiple of 64 (checked by the caller)
+    const dim3 grid((uint32_t)n_rows, (uint32_t)((d + w - 1) / w));
+    if (w == 64)
+        hipLaunchKernelGGL((k_chain_rows<MODE, XD, 64>), grid, dim3(64), 0, s, edges, blocks, rows,
+                           x, xdiv, d, y, ldy, ep);
+    else if (w == 32)
+        hipLaunchKernelGGL((k_chain_rows<MODE, XD, 32>), grid, dim3(64), 0, s, edges, blocks, rows,
+                           x, xdiv, d, y, ldy, ep);
+    else
+        hipLaunchKernelGGL((k_chain_rows<MODE, XD, 16>), grid, dim3(64), 0, s, edges, blocks, rows,
+                           x, xdiv, d, y, ldy, ep);
+    return herr_x(hipGetLastError());
+}
+
+template <int MODE>
+int chain_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+               const lgcn_emu_row_t* rows, int32_t n_rows, const lgcn_rows_t& x, float xdiv,
+               float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
+    // the row mask of X (XD & 4) only saves gathers; the chain reads the (all-zero) dead rows
+    switch (xd & 3) {
+        case 0: return launch_chain<MODE, 0>(edges, blocks, rows, n_rows, x, xdiv, y, ldy, d, ep, s);
+        case 1: return launch_chain<MODE, 1>(edges, blocks, rows, n_rows, x, xdiv, y, ldy, d, ep, s);
+        case 2: return launch_chain<MODE, 2>(edges, blocks, rows, n_rows, x, xdiv, y, ldy, d, ep, s);
+        default: return LGCN_EINVAL;
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -853,6 +1049,43 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
             return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         default:
             return LGCN_EINVAL;
+    }
+}
+
+
+int lgcn_chain_supported(int32_t d) { return d == 16 || d == 32 || (d > 0 && d % 64 == 0); }
+
+int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                    const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
+                    float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                    void* stream) {
+    if (n_rows < 0 || !lgcn_chain_supported(d) || d > 2048 || !(x_div > 0.f) || !epi_host)
+        return LGCN_EINVAL;
+    if (n_rows == 0) return 0;
+    if (!edges || !blocks || !rows || !y || ldy < d || !x.p0) return LGCN_EINVAL;
+    // 16-B row slices: every X segment and the row stride 16-B aligned
+    if (x.ld % 4 || (reinterpret_cast<uintptr_t>(x.p0) & 15) ||
+        (reinterpret_cast<uintptr_t>(x.p1) & 15) || (reinterpret_cast<uintptr_t>(x.p2) & 15))
+        return LGCN_EALIGN;
+    lgcn_epilogue_t ep = *epi_host;
+    if (ep.mode == LGCN_EPI_MEAN && (ep.n_prev < 1 || ep.n_prev - 1 > LGCN_MAX_LAYERS))
+        return LGCN_EINVAL;
+    if (ep.mode == LGCN_EPI_ADD && !ep.addend.p0) return LGCN_EINVAL;
+    if (ep.mode != LGCN_EPI_STORE && !(ep.div > 0.f)) return LGCN_EINVAL;
+    if (ep.mode != LGCN_EPI_STORE && is_pow2(ep.div)) {
+        const float inv = 1.0f / ep.div;
+        memcpy(&ep.pad, &inv, sizeof(inv));
+    } else {
+        ep.pad = 0;
+    }
+    const int xd = xd_of(x_div, nullptr);
+    const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    switch (ep.mode) {
+        case LGCN_EPI_STORE: return chain_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
+        case LGCN_EPI_MEAN: return chain_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
+        case LGCN_EPI_ADD: return chain_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
+        default: return LGCN_EINVAL;
     }
 }
 

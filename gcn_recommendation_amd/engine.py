@@ -24,7 +24,7 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
-ABI_VERSION = 6
+ABI_VERSION = 7
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 32, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -139,6 +139,9 @@ ABI = [
                                        _P]),
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
                                      _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P]),
+    ("lgcn_chain_supported", ctypes.c_int, [_I32]),
+    ("lgcn_chain_rows", ctypes.c_int, [_P, _P, _P, _I32, RowsT, ctypes.c_float, _P, _I64, _I32,
+                                       ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_layer", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, ctypes.c_float, _P,
                                   _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _I32,
@@ -290,15 +293,17 @@ class HubPlan:
         self._split = None
 
     def emu_parts(self, bounds=(4096, 512)):
-        """The emulated rows cut by length into consecutive (row0, row1, block0, block1) groups:
-        rows of more than bounds[0] blocks, then more than bounds[1], then the rest (rows are
-        stored longest first). The longest walks are the critical path of a layer."""
+        """The emulated rows cut by length into consecutive (row0, row1, block0, block1, short)
+        groups: rows of more than bounds[0] blocks, then more than bounds[1], then the rest
+        (rows are stored longest first; short = the last group, whose rows — at most
+        bounds[1] * 256 edges — may run as plain sequential chains, lgcn_chain_rows). The
+        longest walks are the critical path of a layer."""
         if self._split is None:
             nb = self.emu_rows[:, 2].cpu().numpy() if self.n_emu_rows else np.zeros(0, np.int64)
             cuts = [0] + [int((nb > b).sum()) for b in bounds] + [int(nb.size)]
             firsts = np.concatenate([[0], np.cumsum(nb)])
-            self._split = [(r0, r1, int(firsts[r0]), int(firsts[r1]))
-                           for r0, r1 in zip(cuts[:-1], cuts[1:]) if r1 > r0]
+            self._split = [(r0, r1, int(firsts[r0]), int(firsts[r1]), i == len(bounds))
+                           for i, (r0, r1) in enumerate(zip(cuts[:-1], cuts[1:])) if r1 > r0]
         return self._split
 
     @property
@@ -680,6 +685,17 @@ def _side_stream(device, i=0):
     return _side_streams[key]
 
 
+def chain_enabled():
+    """Emulated rows of the short part (<= 512 blocks) run as plain sequential chains
+    (lgcn_chain_rows) instead of block pass + walk; LGCN_CHAIN=0 emulates them too."""
+    return os.environ.get("LGCN_CHAIN", "1") != "0"
+
+
+def _aligned16(segments):
+    return all(t.data_ptr() % 16 == 0 and (t.dim() < 2 or t.stride(0) % 4 == 0)
+               for t in segments)
+
+
 emu_trace = None  # a list: spmm_layer records (name, event) pairs of its streams' phases into it
 
 
@@ -728,6 +744,7 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     # their walk starts as soon as it is done, on a side stream of their own; shorter emulated
     # rows follow on further side streams (rows are stored longest first)
     parts = hp.emu_parts()
+    chain = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
     sides = [_side_stream(graph.device, i) for i in range(len(parts))]
     tr = emu_trace
     if tr is not None:  # diagnostics (tools/exact_layer_probe.py): per-stream phase events
@@ -736,8 +753,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     for sd in sides:
         sd.wait_stream(main)        # X (and the epilogue operands) are ready
     rb, bb = hp.emu_rows.element_size() * 4, hp.emu_blocks.element_size() * 4
-    for sd, (r0, r1, b0, b1) in zip(sides, parts):
-        if r1 <= r0:
+    for sd, (r0, r1, b0, b1, short) in zip(sides, parts):
+        if r1 <= r0 or (short and chain):
             continue
         ss = ctypes.c_void_p(sd.cuda_stream)
         # records are indexed by block: a sub-range of blocks writes at its own offset
@@ -760,8 +777,17 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     if tr is not None:
         tr.append(("layer_kernel", main.record_event(torch.cuda.Event(enable_timing=True))))
     slots = emu_slots()
-    for i, (sd, (r0, r1, b0, b1)) in enumerate(zip(sides, parts)):
+    for i, (sd, (r0, r1, b0, b1, short)) in enumerate(zip(sides, parts)):
         if r1 <= r0:
+            continue
+        if short and chain:
+            _check(lib.lgcn_chain_rows(_ptr(graph.edges), plan.emu_blocks, plan.emu_rows + r0 * rb,
+                                       r1 - r0, x, x_div, _ptr(y), y.stride(0), d,
+                                       ctypes.byref(epi), ctypes.c_void_p(sd.cuda_stream)),
+                   "lgcn_chain_rows")
+            if tr is not None:
+                tr.append((f"part{i}_chain", sd.record_event(
+                    torch.cuda.Event(enable_timing=True))))
             continue
         _check(lib.lgcn_emu_walk(_ptr(graph.edges), plan.emu_blocks, plan.emu_rows + r0 * rb,
                                  r1 - r0, plan.emu_rel, plan.emu_meta, plan.emu_stage, x, x_div,

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 6
+#define LGCN_ABI_VERSION 7
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -307,6 +307,18 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
                   void* stream);
+
+/* Mid-size emulated rows run as the reference's sequential chain itself (no block pass): one
+ * wave per (row, column slice) folds acc = fma(val_j, X[col_j, c], acc) in stored order from +0
+ * while the next windows of gathered X rows are in flight by LDS-DMA. rows / blocks: as for
+ * lgcn_emu_walk (a row's edges are [blocks[first].beg, blocks[first + n - 1].end)). X rows and
+ * segments 16-B aligned; d: lgcn_chain_supported(d) (16, 32 or a multiple of 64). x_nz is not
+ * taken: dead rows of a row-sparse X are all zero, and folding them is exact. */
+int lgcn_chain_supported(int32_t d);
+int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                    const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
+                    float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                    void* stream);
 
 /* One whole layer under a hub plan: emulation block pass, lgcn_spmm_layer (bundles, chunks and
  * long rows), chunk combine, emulation walk — every row of Y written once. */

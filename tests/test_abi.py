@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 6
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 7
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -85,6 +85,12 @@ def test_argument_validation_without_gpu(lib):
                              ctypes.byref(ep), 0, None) == -1
     assert lib.lgcn_emu_walk(None, None, None, 0, None, None, None, rows, 1.0, None, None, 64, 64,
                              ctypes.byref(ep), 64, None) == -1   # slots out of range
+    assert [lib.lgcn_chain_supported(d) for d in (8, 16, 24, 32, 64, 128, 192, 256)] == \
+        [0, 1, 0, 1, 1, 1, 1, 1]
+    assert lib.lgcn_chain_rows(None, None, None, 0, rows, 1.0, None, 64, 64, ctypes.byref(ep),
+                               None) == 0     # nothing to do
+    assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 24, ctypes.byref(ep),
+                               None) == -1    # unsupported width
     assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 0
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,

@@ -1,5 +1,6 @@
-"""GPU parity of the exact hub path — hub rows reproduced by block emulation
-(gcn_recommendation_amd/csrc/lgcn_exact.hip) — against the oracle's sequential fmaf chain
+"""GPU parity of the exact hub path — hub rows reproduced by block emulation, and the shorter
+of them (<= 512 blocks) by the latency-hidden sequential chain (LGCN_CHAIN=1, the default;
+both in gcn_recommendation_amd/csrc/lgcn_exact.hip) — against the oracle's sequential fmaf chain
 (oracle/lgcn_oracle.c, the arithmetic of models/lightgcn.py:45's torch.sparse.mm on CPU).
 
 Bar: BITWISE, forward and backward, for every input. The cases aim at the emulation's proof
@@ -50,10 +51,12 @@ def _adj(r, c, v, n, dev):
                                    (n, n)).to(dev)
 
 
+@pytest.mark.parametrize("chain", ["1", "0"])
 @pytest.mark.parametrize("order", ["degree", "stored"])
 @pytest.mark.parametrize("kind", ["xavier", "drift", "few_bits", "range", "sparse_rows"])
-def test_emulated_hubs_bitwise(gpu_device, monkeypatch, kind, order):
+def test_emulated_hubs_bitwise(gpu_device, monkeypatch, kind, order, chain):
     monkeypatch.setenv("LGCN_ROW_ORDER", order)
+    monkeypatch.setenv("LGCN_CHAIN", chain)
     rng = np.random.default_rng(11)
     r, c, v, n = _powerlaw(rng, 40_000, 3_000, 200_000)
     g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device))
@@ -73,8 +76,10 @@ def test_emulated_hubs_bitwise(gpu_device, monkeypatch, kind, order):
         assert np.array_equal(got_b.view(np.uint32), want_b.view(np.uint32)), (kind, sparse)
 
 
+@pytest.mark.parametrize("chain", ["1", "0"])
 @pytest.mark.parametrize("d", [1, 8, 12, 16, 32, 100, 128, 256])
-def test_emulated_hubs_widths(gpu_device, d):
+def test_emulated_hubs_widths(gpu_device, monkeypatch, d, chain):
+    monkeypatch.setenv("LGCN_CHAIN", chain)
     rng = np.random.default_rng(100 + d)
     r, c, v, n = _powerlaw(rng, 8_000, 600, 40_000)
     g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device))
@@ -86,9 +91,12 @@ def test_emulated_hubs_widths(gpu_device, d):
         assert np.array_equal(got.cpu().numpy(), want), (d, K)
 
 
-def test_one_giant_row(gpu_device):
+@pytest.mark.parametrize("chain", ["1", "0"])
+def test_one_giant_row(gpu_device, monkeypatch, chain):
     """A 300k-edge item row (1,172 blocks: several 64-block walker chunks), first block ragged
-    by the planner's cut, plus a row of exactly 256 and 257 edges."""
+    by the planner's cut, plus a row of exactly 256 and 257 edges (sequential chains: one
+    window + a partial one, and the ring's dummy windows past the row)."""
+    monkeypatch.setenv("LGCN_CHAIN", chain)
     rng = np.random.default_rng(3)
     U = 300_000
     users = np.concatenate([np.arange(U), rng.integers(0, U, 256), rng.integers(0, U, 257),
