@@ -813,12 +813,6 @@ __device__ __forceinline__ void lds_read16(uint32_t a, float (&v)[16]) {
         : "memory");
 }
 
-__device__ __forceinline__ float lds_read1(uint32_t a) {
-    float v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-    return v;
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -887,24 +881,33 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
         rec_dma(w + 2 * AHEAD);
         const int n = min(64, end - beg - 64 * w);
         const uint32_t xa = lds_addr(&s_x[w % NX][cc]);
-        const float vme = lds_read1(lds_addr(&s_rec[w % NR][lane].y));  // lane j: val of edge j
-#define LGCN_CHAIN_FOLD(G)                                                                    \
+        const uint32_t va = lds_addr(&s_rec[w % NR][0].y);  // same address in every lane
+        // 16 steps at a time: X elements and (broadcast) edge values from LDS, then the chain;
+        // only the row's last window is partial (steps past n leave acc alone)
+#define LGCN_CHAIN_FOLD(G, FULL)                                                              \
         {                                                                                     \
-            float xv[16];                                                                     \
+            float xv[16], vv[16];                                                             \
             lds_read16<(G) * W * 4, W * 4>(xa, xv);                                           \
+            lds_read16<(G) * 8, 8>(va, vv);                                                   \
             _Pragma("unroll") for (int t = 0; t < 16; ++t) {                                  \
                 float xe = xv[t];                                                             \
                 if constexpr ((XD & 3) == 1) xe = xe / xdiv;                                  \
                 else if constexpr ((XD & 3) == 2) xe = xe * xdiv;                             \
-                const float v = __int_as_float(                                               \
-                    __builtin_amdgcn_readlane(__float_as_int(vme), (G) + t));                 \
-                acc = (G) + t < n ? __builtin_fmaf(v, xe, acc) : acc;                         \
+                if (FULL) acc = __builtin_fmaf(vv[t], xe, acc);                               \
+                else acc = (G) + t < n ? __builtin_fmaf(vv[t], xe, acc) : acc;                \
             }                                                                                 \
         }
-        LGCN_CHAIN_FOLD(0)
-        LGCN_CHAIN_FOLD(16)
-        LGCN_CHAIN_FOLD(32)
-        LGCN_CHAIN_FOLD(48)
+        if (n == 64) {
+            LGCN_CHAIN_FOLD(0, true)
+            LGCN_CHAIN_FOLD(16, true)
+            LGCN_CHAIN_FOLD(32, true)
+            LGCN_CHAIN_FOLD(48, true)
+        } else {
+            LGCN_CHAIN_FOLD(0, false)
+            LGCN_CHAIN_FOLD(16, false)
+            LGCN_CHAIN_FOLD(32, false)
+            LGCN_CHAIN_FOLD(48, false)
+        }
 #undef LGCN_CHAIN_FOLD
     }
     wait_vm<0>();  // no LDS-DMA may land after the wave (and its LDS) is gone
