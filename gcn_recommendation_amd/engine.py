@@ -291,6 +291,7 @@ class HubPlan:
         self.n_emu_rows = 0 if emu_rows is None else emu_rows.shape[0]
         self._scratch = {}
         self._split = None
+        self._split_bounds = None
 
     def emu_parts(self, bounds=(4096, 512)):
         """The emulated rows cut by length into consecutive (row0, row1, block0, block1, short)
@@ -298,12 +299,13 @@ class HubPlan:
         (rows are stored longest first; short = the last group, whose rows — at most
         bounds[1] * 256 edges — may run as plain sequential chains, lgcn_chain_rows). The
         longest walks are the critical path of a layer."""
-        if self._split is None:
+        if self._split is None or self._split_bounds != bounds:
             nb = self.emu_rows[:, 2].cpu().numpy() if self.n_emu_rows else np.zeros(0, np.int64)
             cuts = [0] + [int((nb > b).sum()) for b in bounds] + [int(nb.size)]
             firsts = np.concatenate([[0], np.cumsum(nb)])
             self._split = [(r0, r1, int(firsts[r0]), int(firsts[r1]), i == len(bounds))
                            for i, (r0, r1) in enumerate(zip(cuts[:-1], cuts[1:])) if r1 > r0]
+            self._split_bounds = bounds
         return self._split
 
     @property
@@ -680,7 +682,7 @@ def _side_stream(device, i=0):
     (LGCN_EMU_PRIORITY=0: normal) so its waves are dispatched ahead of the layer kernel's."""
     key = (str(device), i)
     if key not in _side_streams:
-        hi = i == 0 and os.environ.get("LGCN_EMU_PRIORITY", "1") != "0"
+        hi = i < int(os.environ.get("LGCN_EMU_PRIORITY", "1"))  # streams 0..n-1 high priority
         _side_streams[key] = torch.cuda.Stream(device, priority=-1 if hi else 0)
     return _side_streams[key]
 
@@ -743,7 +745,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     # the longest rows' walks are the critical path: their block pass runs first, alone, and
     # their walk starts as soon as it is done, on a side stream of their own; shorter emulated
     # rows follow on further side streams (rows are stored longest first)
-    parts = hp.emu_parts()
+    parts = hp.emu_parts(tuple(int(b) for b in os.environ.get(
+        "LGCN_EMU_PART_BOUNDS", "4096,512").split(",")))
     chain = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
     sides = [_side_stream(graph.device, i) for i in range(len(parts))]
     tr = emu_trace
