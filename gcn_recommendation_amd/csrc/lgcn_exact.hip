@@ -778,8 +778,11 @@ struct ChainCfg {
     static constexpr int RPI = 64 / LPR;    // rows per 1-KB LDS-DMA instruction
     static constexpr int NI = 64 / RPI;     // instructions per 64-edge window
     static constexpr int XWIN = 64 * W;     // floats per X window
-    static constexpr int NX = 4;            // X windows in the ring (3 in flight while folding)
-    static constexpr int NR = 7;            // record windows in the ring
+    // X windows in flight while one is folded: as many as vmcnt (<= 63 outstanding) allows
+    // with NI + 2 loads per window (W=64: 3 x 18, W=32: 6 x 10, W=16: 8 x 6)
+    static constexpr int AHEAD = W == 64 ? 3 : W == 32 ? 6 : 8;
+    static constexpr int NX = AHEAD + 1;    // X windows in the ring
+    static constexpr int NR = 2 * AHEAD + 1;  // record windows in the ring
 };
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -827,7 +830,8 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
                                                    float* __restrict__ y, int64_t ldy,
                                                    lgcn_epilogue_t ep) {
     using C = ChainCfg<W>;
-    constexpr int NX = C::NX, NR = C::NR, AHEAD = NX - 1;  // X windows in flight
+    constexpr int NX = C::NX, NR = C::NR, AHEAD = C::AHEAD;
+    static_assert(AHEAD * (C::NI + 2) <= 63, "vmcnt holds at most 63 outstanding loads");
     __shared__ __attribute__((aligned(16))) float s_x[NX][C::XWIN];
     __shared__ __attribute__((aligned(16))) int2 s_rec[NR][64];
     const int lane = threadIdx.x;
@@ -933,12 +937,11 @@ template <int MODE, int XD>
 int launch_chain(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                  const lgcn_emu_row_t* rows, int32_t n_rows, const lgcn_rows_t& x, float xdiv,
                  float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
-    const int w = d % 64 == 0 ? 64 : d;  // 16, 32 or a multiple of 64 (checked by the caller)
+    // 128-B slices (one line per gathered row piece) for every d that is a multiple of 32: two
+    // or more waves per row, each with twice the windows in flight of a 64-column wave
+    const int w = d % 32 == 0 ? 32 : 16;  // 16, 32 or a multiple of 64 (checked by the caller)
     const dim3 grid((uint32_t)n_rows, (uint32_t)((d + w - 1) / w));
-    if (w == 64)
-        hipLaunchKernelGGL((k_chain_rows<MODE, XD, 64>), grid, dim3(64), 0, s, edges, blocks, rows,
-                           x, xdiv, d, y, ldy, ep);
-    else if (w == 32)
+    if (w == 32)
         hipLaunchKernelGGL((k_chain_rows<MODE, XD, 32>), grid, dim3(64), 0, s, edges, blocks, rows,
                            x, xdiv, d, y, ldy, ep);
     else

@@ -746,7 +746,7 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     # their walk starts as soon as it is done, on a side stream of their own; shorter emulated
     # rows follow on further side streams (rows are stored longest first)
     parts = hp.emu_parts(tuple(int(b) for b in os.environ.get(
-        "LGCN_EMU_PART_BOUNDS", "4096,512").split(",")))
+        "LGCN_EMU_PART_BOUNDS", "8192,1024").split(",")))  # probe: 4096,512 -> 8192,1024: -1.1 ms
     chain = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
     sides = [_side_stream(graph.device, i) for i in range(len(parts))]
     tr = emu_trace
