@@ -26,6 +26,7 @@ int g_rows_per_group = 0;
 int g_unroll = 0;
 int g_mean_prefetch = 0;
 int g_min_groups = 0;
+int g_emu_resolve = 0;  // LGCN_TUNE_EMU_RESOLVE (read by lgcn_exact.hip's walk launch)
 }  // namespace lgcn_detail
 
 namespace {
@@ -369,6 +370,11 @@ int lgcn_tune(int knob, int value) {
         case LGCN_TUNE_MIN_GROUPS: {
             const int old = lgcn_detail::g_min_groups;
             if (value >= 0) lgcn_detail::g_min_groups = value;
+            return old;
+        }
+        case LGCN_TUNE_EMU_RESOLVE: {
+            const int old = lgcn_detail::g_emu_resolve;
+            if (value >= 0) lgcn_detail::g_emu_resolve = value;
             return old;
         }
         default:

@@ -8,48 +8,62 @@
 // without running it step by step.
 //
 // Translation invariance. Let e be a binade (|a| in [2^e, 2^(e+1))) and u = 2^(e-23) its ulp.
-// If a chain value a is a multiple of u and a + p stays inside binade e, then
-// fma-rounding gives RN(a + p) = a + RN_u(p) (RN_u: nearest multiple of u; the tie case depends
-// on a's parity). So two chains over the same steps, started from a and a' in binade e, stay
-// exactly a - a' apart as long as both trajectories stay inside the binade (and no step is an
-// exact tie). Hence:
+// If a chain value a is a multiple of u and the exact a + p lies inside binade e, fma-rounding
+// gives RN(a + p) = a + RN_u(p) (RN_u: nearest multiple of u; only an exact tie would depend on
+// a's parity). RN_u(p) does not depend on a — nor on a's SIGN. So along a stretch of steps whose
+// results all stay inside binade e, the chain is an integer prefix sum: in units of u its
+// magnitude mantissa M moves by +-q_j, q_j = RN_u(p_j) / u. Hence:
 //   * k_emu_blocks cuts a hub row into blocks of <= 256 edges. For each (block, column) it runs
-//     32 CANDIDATE chains from a' = +-1.5 * 2^e, e in a 16-binade window chosen from the block's
-//     own first products, and records rel = chain_end - a' (exact), bounds lo/hi on the exact
-//     running sum of its products (from the block's own chain from +0, widened by its rounding
-//     error; every trajectory of the block stays within 128 ulps of that sum), and the largest
-//     lowest-set-bit exponent of its products (a product can be an exact tie only if that
-//     exponent reaches e - 24). Block 0 of a row keeps its chain from +0: the true value.
-//   * k_emu_walk (one wave per (row, column)) walks the blocks in order with the true value a:
-//     if a's binade has a candidate, both trajectories provably stay inside it and no tie is
-//     possible, a += rel (exact); otherwise the block is re-run as the sequential fma chain.
-// Every step is therefore either the reference's own fma or a proven-identical translation:
-// the result is bitwise the reference's, whatever the data (ties, zero crossings, subnormals,
-// inf/NaN all take the sequential path). oracle/lgcn_oracle.c holds the sequential chain the
-// tests compare against; DESIGN.md §3 has the argument and the measured slow-block fractions.
+//     16 CANDIDATE chains from +1.5 * 2^e, e in a 16-binade window chosen from the block's own
+//     first products; candidate e's end minus its start is K_e = sum_j q_j (exact, when the
+//     candidate stayed in its binade). It records K_e, bounds on the block's exact running sum
+//     (from its own chain from +0, widened by that chain's rounding: every trajectory of the
+//     block stays within 128 ulps of it) and a per-binade validity mask (candidate inside its
+//     binade, bounds representable, and no product able to be an exact tie at ulp u_e: the
+//     lowest set bit of every product lies below u_e / 2). Block 0 of a row keeps its chain from
+//     +0: the true value. It also stages the block's X elements per column (and the edge
+//     values), so a block the walk must resolve is one contiguous 2-KB fetch.
+//   * k_emu_walk (one wave per (row, column)) walks the blocks in order with the true value a,
+//     64 blocks per scan (lane = block): a DPP prefix sum of the translations gives every lane
+//     its start mantissa if all earlier blocks translate, and each lane tests that its whole
+//     trajectory stays inside the binade. The first block that fails is RESOLVED IN PARALLEL:
+//     lane l holds steps 4l..4l+3, computes q_j = (fma(v_j, x_j, C) - C) / u with C = 1.5 * 2^e
+//     (exact, C's binade is e), a wave prefix sum gives the magnitude after every step, and the
+//     first step whose result could leave the binade (or whose product could be a tie) is done
+//     as the reference's own fma; the scan restarts after it in the new binade. A block costs
+//     one scan per binade change instead of 256 dependent FMAs.
+// Every step is therefore either the reference's own fma or a proven-identical integer step:
+// the result is bitwise the reference's, whatever the data (zero, subnormal, inf and NaN values
+// take the sequential fma). oracle/lgcn_oracle.c holds the sequential chain the tests compare
+// against; DESIGN.md §3 has the argument and the measured decision mix.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
 #include "lgcn.h"
 
+namespace lgcn_detail {
+extern int g_emu_resolve;  // LGCN_TUNE_EMU_RESOLVE (lgcn_engine.hip)
+}
+
 namespace {
 
-constexpr int kW = LGCN_EMU_CANDS / 2;  // binades per sign
-constexpr int kEOff = 2;                // window starts 2 binades above the first 64 steps' reach
-constexpr int16_t kIdentity = -32768;   // maxlsb sentinel: no nonzero product in the block
-constexpr int16_t kNoFast = 32000;      // maxlsb sentinel: never take the fast path
-constexpr int kSlack = 132;             // ulps: 128 for <= 256 steps of <= 1/2 ulp + margin
+constexpr int kNB = LGCN_EMU_CANDS;           // binades per (block, column) table
+constexpr int kEOff = 2;                      // window starts 2 binades above the first 64 steps' reach
+constexpr int kSlack = 132;                   // ulps: 128 for <= 256 steps of <= 1/2 ulp + margin
+constexpr int kLB = (1 << 23) + kSlack;       // a trajectory's mantissa must stay in [kLB, kHB]
+constexpr int kHB = (1 << 24) - kSlack;
+constexpr int kC = 3 << 22;                   // a candidate's start mantissa (1.5 * 2^23)
+constexpr int kIdentEb = -32768;              // meta ebase of a block without a nonzero product
+static_assert(kNB == 16, "tables hold 16 binades (4 x int4 per (block, column))");
+static_assert(LGCN_EMU_META_BYTES == 16, "meta record is one int4");
 
-struct EmuMeta {
-    int32_t lo;      // floor(L * 2^(23 - ebase)), L a lower bound of the block's exact running sum
-    int32_t hi;      // ceil(H * 2^(23 - ebase)), H an upper bound
-    int16_t ebase;   // binade of candidate pair 0
-    int16_t maxlsb;  // max over nonzero products of the exponent of their lowest set bit
-                     // (kIdentity: no nonzero product; kNoFast: bounds too wide for int32)
-    float r0;        // block 0 of a row: the exact chain from +0
-};
-static_assert(sizeof(EmuMeta) == LGCN_EMU_META_BYTES, "meta record size");
+// Records written by k_emu_blocks per (block, column) rc = block * d + column:
+//   meta[rc] = int4 {lo0, hi0, pk, r0}: lo0 / hi0 = floor / ceil of bounds on the block's exact
+//     running sum in units of u_ebase; pk = ebase (low 16 bits, signed; kIdentEb: every product
+//     is zero) | valid mask << 16 (bit w: binade ebase + w may translate); r0 = bits of the
+//     block's chain from +0 (the true chain for block 0 of a row);
+//   ktab[4 rc .. 4 rc + 3] = int4 x 4: K[w], the translation of binade ebase + w in its ulps.
 
 __device__ __forceinline__ const float* seg_row_x(const lgcn_rows_t& s, int32_t r) {
     if (r < s.end0) return s.p0 + (int64_t)r * s.ld;
@@ -100,6 +114,11 @@ __device__ __forceinline__ int lsb_exp(float f) {
     return E - 150 + __builtin_ctz(M | 0x800000u);
 }
 
+// lowest-set-bit exponent of the exact product v * x (-100000: the product is zero)
+__device__ __forceinline__ int lsb_exp_prod(float v, float x) {
+    return (v != 0.f && x != 0.f) ? lsb_exp(v) + lsb_exp(x) : -100000;
+}
+
 // ---------------------------------------------------------------------------------------------
 // block pass: one wave per (block, 64-column slice); lane = column
 // ---------------------------------------------------------------------------------------------
@@ -108,8 +127,8 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                                                    const lgcn_emu_block_t* __restrict__ blocks,
                                                    lgcn_rows_t x, float xdiv,
                                                    const uint32_t* __restrict__ x_nz, int32_t d,
-                                                   int32_t* __restrict__ rel,
-                                                   EmuMeta* __restrict__ meta,
+                                                   int4* __restrict__ ktab,
+                                                   int4* __restrict__ meta,
                                                    float* __restrict__ stage) {
     constexpr int SW = 16;  // steps gathered per sub-window (all in flight at once)
     const int lane = threadIdx.x;
@@ -118,10 +137,10 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     const lgcn_emu_block_t blk = blocks[blockIdx.x];
     // T: the sequential fma chain of the block from +0. It is the true chain for block 0; for
     // every block it tracks the exact running sum S of the products to within 1/2 ulp(|T|) per
-    // step, which bounds every trajectory of the block (EmuMeta lo/hi)
+    // step, which bounds every trajectory of the block (meta lo0/hi0)
     float T = 0.f, tlo = 0.f, thi = 0.f;
     int maxlsb = -100000;
-    float cand[LGCN_EMU_CANDS];
+    float cand[kNB];
     bool init = false;
     int ebase = 0;
     const int cc = act ? c : d - 1;  // lanes past d load a valid element and mask it
@@ -139,9 +158,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             xv[t] = load_elem<XD>(x, x_nz, col, cc, xdiv, act && s0 + t < n);
         }
     };
-    // one sub-window: steps past the block end read as (0, 0), and fma(0, 0, c) == c for every
-    // chain value (a chain is never -0), so the unrolled steps need no guard
-    // this (block, column)'s elements, in step order (the walk re-runs a block from here)
+    // this (block, column)'s elements, in step order (the walk resolves a block from here)
     // stage layout [block][d + 1][BLOCK]: column c's X elements, then (column d) the edge values
     float* st = stage ? stage + ((int64_t)blockIdx.x * (d + 1) + cc) * LGCN_EMU_BLOCK : nullptr;
     float* sv = stage && blockIdx.y == 0
@@ -153,6 +170,8 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             *reinterpret_cast<float4*>(st + step0 + 4 * q) =
                 make_float4(xv[4 * q], xv[4 * q + 1], xv[4 * q + 2], xv[4 * q + 3]);
     };
+    // one sub-window: steps past the block end read as (0, 0), and fma(0, 0, c) == c for every
+    // chain value (a chain is never -0), so the unrolled steps need no guard
     auto run_sub = [&](const float (&xv)[SW], const float (&vv)[SW]) {
         if (!init) {
             // candidates start at the first sub-window holding a nonzero product (before it the
@@ -170,10 +189,9 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                 frexpf(m, &e);
                 ebase = max(-200, min(e - 1 + kEOff + 1, 200));  // 16 steps reach ~1/2 of 64
 #pragma unroll
-                for (int k = 0; k < LGCN_EMU_CANDS; ++k) {
-                    const int eb = ebase + (k >> 1);
-                    const float a0 = (eb >= -126 && eb <= 127) ? ldexpf(1.5f, eb) : 1.5f;
-                    cand[k] = (k & 1) ? -a0 : a0;
+                for (int k = 0; k < kNB; ++k) {
+                    const int eb = ebase + k;
+                    cand[k] = (eb >= -126 && eb <= 127) ? ldexpf(1.5f, eb) : 1.5f;
                 }
             }
         }
@@ -182,15 +200,13 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             T = __builtin_fmaf(vv[t], xv[t], T);
             tlo = fminf(tlo, T);
             thi = fmaxf(thi, T);
-            const int le = lsb_exp(vv[t]) + lsb_exp(xv[t]);
-            maxlsb = (vv[t] != 0.f && xv[t] != 0.f) ? max(maxlsb, le) : maxlsb;
+            maxlsb = max(maxlsb, lsb_exp_prod(vv[t], xv[t]));
         }
         if (init) {
 #pragma unroll
             for (int t = 0; t < SW; ++t) {
 #pragma unroll
-                for (int k = 0; k < LGCN_EMU_CANDS; ++k)
-                    cand[k] = __builtin_fmaf(vv[t], xv[t], cand[k]);
+                for (int k = 0; k < kNB; ++k) cand[k] = __builtin_fmaf(vv[t], xv[t], cand[k]);
             }
         }
     };
@@ -218,23 +234,6 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     }
     if (!act) return;
     const int64_t rc = (int64_t)blockIdx.x * d + c;
-    // candidate k's translation in units of its ulp u_k = 2^(ebase + k/2 - 23): exact integer
-    // when the candidate's chain stayed in its binade (the walker checks exactly that)
-    int4* rp = reinterpret_cast<int4*>(rel + rc * LGCN_EMU_CANDS);
-#pragma unroll
-    for (int q = 0; q < LGCN_EMU_CANDS / 4; ++q) {
-        int r4[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int k = 4 * q + t;
-            const int eb = ebase + (k >> 1);
-            const float a0 = (eb >= -126 && eb <= 127) ? ldexpf(1.5f, eb) : 1.5f;
-            const float dlt = cand[k] - ((k & 1) ? -a0 : a0);
-            const float ku = ldexpf(dlt, 23 - eb);
-            r4[t] = (init && fabsf(ku) < 16777216.f) ? (int)ku : 0;
-        }
-        rp[q] = make_int4(r4[0], r4[1], r4[2], r4[3]);
-    }
     // |T_j - S_j| <= j * ulp(max|T|) / 2 <= 128 * ulp(max|T|) for a block of <= 256 steps
     const float M = fmaxf(-tlo, thi);
     double err = 0.0;
@@ -246,125 +245,47 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     const double lo_u = floor(ldexp((double)tlo - err, 23 - ebase));
     const double hi_u = ceil(ldexp((double)thi + err, 23 - ebase));
     const bool fits = lo_u >= -1073741824.0 && hi_u <= 1073741824.0;
-    EmuMeta m;
-    m.lo = fits ? (int32_t)lo_u : 0;
-    m.hi = fits ? (int32_t)hi_u : 0;
-    m.ebase = (int16_t)ebase;
-    m.maxlsb = (maxlsb == -100000) ? kIdentity
-               : !fits ? kNoFast : (int16_t)max(-32000, min(maxlsb, 31999));
-    m.r0 = T;
-    meta[rc] = m;
+    const int32_t lo0 = fits ? (int32_t)lo_u : 0, hi0 = fits ? (int32_t)hi_u : 0;
+    // candidate k: translation in units of its ulp u_k = 2^(ebase + k - 23) — an exact integer
+    // when the candidate's chain stayed in its binade, which the validity bit certifies
+    uint32_t vm = 0;
+    int K[kNB];
+#pragma unroll
+    for (int k = 0; k < kNB; ++k) {
+        const int eb = ebase + k;
+        const bool normal = eb >= -126 && eb <= 127;
+        const float a0 = normal ? ldexpf(1.5f, eb) : 1.5f;
+        const float ku = ldexpf(cand[k] - a0, 23 - eb);
+        const bool kfit = fabsf(ku) < 16777216.f;
+        K[k] = (init && kfit) ? (int)ku : 0;
+        const int lo = lo0 >> k, hi = -((-hi0) >> k);
+        const bool ok = init && fits && normal && kfit && kC + lo >= kLB && kC + hi <= kHB &&
+                        maxlsb < eb - 24;
+        vm |= ok ? (1u << k) : 0u;
+    }
+    const bool ident = maxlsb == -100000;
+    const int pk = ident ? (kIdentEb & 0xffff) : (int)(((uint32_t)ebase & 0xffffu) | (vm << 16));
+    meta[rc] = make_int4(lo0, hi0, pk, __float_as_int(T));
+    int4* kp = ktab + rc * 4;
+#pragma unroll
+    for (int q = 0; q < kNB / 4; ++q)
+        kp[q] = make_int4(K[4 * q], K[4 * q + 1], K[4 * q + 2], K[4 * q + 3]);
 }
 
 // ---------------------------------------------------------------------------------------------
 // walker: one wave per (hub row, column). The chain value is wave-uniform.
 // ---------------------------------------------------------------------------------------------
-// A block the walk re-runs as the reference does: a = fma(val_j, x_j, a) in stored order.
-// SlowData holds one lane's share of a block's (val, x) pairs, fetched with every load in
-// flight at once: x from the staged copy (contiguous) or gathered from X (a second round trip).
-struct SlowData {
-    int2 rec[LGCN_EMU_BLOCK / 64];   // edge records of steps t * 64 + lane
-    float xg[LGCN_EMU_BLOCK / 64];   // gathered x of the same steps (no stage)
-    float4 xs;                       // staged x of steps 4 * lane .. 4 * lane + 3
-};
-
-template <int XD>
-__device__ __forceinline__ void slow_load(SlowData& sd, const lgcn_edge_t* __restrict__ edges,
-                                          int32_t beg, int32_t end, const lgcn_rows_t& x,
-                                          float xdiv, const uint32_t* __restrict__ x_nz,
-                                          const float* __restrict__ st, int c) {
-    constexpr int Q = LGCN_EMU_BLOCK / 64;
-    const int lane = threadIdx.x;
-    const int n = end - beg;
-#pragma unroll
-    for (int t = 0; t < Q; ++t)  // clamped addresses, masked values: all loads in flight
-        sd.rec[t] = *reinterpret_cast<const int2*>(edges + beg + min(t * 64 + lane, n - 1));
-    if (st) {
-        sd.xs = *reinterpret_cast<const float4*>(st + 4 * lane);
-    } else {
-#pragma unroll
-        for (int t = 0; t < Q; ++t)
-            sd.xg[t] = load_elem<XD>(x, x_nz, sd.rec[t].x, c, xdiv, t * 64 + lane < n);
-    }
-}
-
-// LDS ordering point for the walker (a one-wave workgroup: a wave's LDS operations complete in
-// order, so only the compiler must not move LDS accesses across this point). __syncthreads()
-// would also make the compiler drain every global load in flight (vmcnt(0)) — the prefetched
-// re-run blocks and the next chunk's records — exposing their latency at every re-run block.
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// A re-run block's (val, x) pairs from a SlowData slot to LDS (sq[step] = (val, x)).
-__device__ __forceinline__ void slow_stage(const SlowData& sd, int n, bool staged, float2* sq) {
-    constexpr int Q = LGCN_EMU_BLOCK / 64;
-    const int lane = threadIdx.x;
-    wave_lds_sync();  // the previous chain's reads of sq are done
-#pragma unroll
-    for (int t = 0; t < Q; ++t) {
-        const bool in = t * 64 + lane < n;
-        sq[t * 64 + lane] = make_float2(in ? __int_as_float(sd.rec[t].y) : 0.f,
-                                        staged ? 0.f : sd.xg[t]);
-    }
-    if (staged) {
-        wave_lds_sync();
-        const float xv[4] = {sd.xs.x, sd.xs.y, sd.xs.z, sd.xs.w};
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (4 * lane + t < n) sq[4 * lane + t].y = xv[t];
-    }
-    wave_lds_sync();
-}
-
-// The sequential chain over a staged block: a = fma(val_j, x_j, a), j = 0 .. n-1.
-__device__ __forceinline__ float slow_chain(int n, float a, const float2* sq) {
-    int i = 0;
-    if (n == LGCN_EMU_BLOCK) {
-        // full block: the LDS reads run PF groups of 8 steps ahead of the FMAs, so only the
-        // dependent FMA chain is on the critical path
-        constexpr int NG = LGCN_EMU_BLOCK / 8, PF = 4;
-        float4 w[PF][4];
-#pragma unroll
-        for (int g = 0; g < PF; ++g)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) w[g][k] = reinterpret_cast<const float4*>(sq + 8 * g)[k];
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            float4 cur[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = w[g % PF][k];
-            if (g + PF < NG) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    w[g % PF][k] = reinterpret_cast<const float4*>(sq + 8 * (g + PF))[k];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                a = __builtin_fmaf(cur[k].x, cur[k].y, a);
-                a = __builtin_fmaf(cur[k].z, cur[k].w, a);
-            }
-        }
-        return a;
-    }
-    for (; i + 8 <= n; i += 8) {
-        float2 w[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = sq[i + k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a = __builtin_fmaf(w[k].x, w[k].y, a);
-    }
-    for (; i < n; ++i) a = __builtin_fmaf(sq[i].x, sq[i].y, a);
-    return a;
-}
-
-// LGCN_EMU_STATS builds (diagnostics only, tools/exact_probe.py): walker decision counters
-// [fast, slow, identity, slow: zero/subnormal, slow: window, slow: tie, slow: bounds, slow steps]
+// LGCN_EMU_STATS builds (diagnostics only, tools/exact_probe.py): walker counters
+// [translated blocks, resolved blocks, identity blocks, not predicted, resolve iterations,
+//  sequential steps, -, -]
 #ifdef LGCN_EMU_STATS
 __device__ unsigned long long g_emu_stats[8];
-// per emulated row (first 256 rows): fast blocks, slow blocks, cycles in slow blocks, max cycles
+// per emulated row (first 256 rows): translated, resolved, cycles resolving, max wave cycles
 __device__ unsigned long long g_emu_row_stats[256][4];
 #endif
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
-// timing experiments only: 1 = re-run blocks skip their chain, 2 = every block translates
+// timing experiments only: 1 = failing blocks are not resolved (value kept), 2 = every block
+// translates
 __device__ int g_emu_mode;
 #define LGCN_EMU_FORCE(f) do { if (g_emu_mode == 2) (f) = true; } while (0)
 #else
@@ -372,58 +293,29 @@ __device__ int g_emu_mode;
 #endif
 #ifdef LGCN_EMU_STATS
 // phase timer of the walker wave (row 0, column 0): s_memtime deltas per phase, then counts
-// [stage, predict, fetch+wait, scans, chains, on-demand fetch, -, -, chunks, predicted, re-run,
-//  not predicted]
+// [tables, predict, slot wait, scans, resolve, on-demand fetch, -, -, chunks, predicted,
+//  resolved, not predicted, resolve iterations]
 __device__ unsigned long long g_emu_phase[16];
 #define PH_MARK(k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
                         ph[k] += now_ - ph_last; ph_last = now_; } while (0)
 #define PH_COUNT(k, v) (ph[k] += (v))
-#else
-#define PH_MARK(k) ((void)0)
-#define PH_COUNT(k, v) ((void)0)
-#endif
-#ifdef LGCN_EMU_STATS
 #define EMU_STAT(k, v) \
     do { if (threadIdx.x == 0) atomicAdd(&g_emu_stats[k], (unsigned long long)(v)); } while (0)
 #else
+#define PH_MARK(k) ((void)0)
+#define PH_COUNT(k, v) ((void)0)
 #define EMU_STAT(k, v) ((void)0)
 #endif
 
-// Fast-path test (k_emu_walk): with e = binade(a), u = 2^(e-23), M = the integer mantissa
-// (a = +-M u, 2^23 <= M < 2^24) and [lo, hi] the block's bounds in units of u, every trajectory
-// value a + (c_j - a) stays in [2^e + u, 2^(e+1) - u] iff its mantissa stays in
-// [2^23 + 1, 2^24 - 1]; kSlack covers the per-step rounding drift. For a < 0 the magnitude moves
-// by -[lo, hi]. The candidate's own chain (from +-1.5 * 2^e) must pass the same test.
-
-// The walk over one row for one column, 64 blocks at a time. Records are staged per chunk of 64
-// blocks: while a chunk is walked, the next one's raw records are loaded into registers; at the
-// chunk boundary they go to LDS together with, for every (block, candidate), the range of start
-// mantissas the candidate's translation is valid for (the bounds test above, precomputed by all
-// 64 lanes). Within a chunk the walk is a SPECULATIVE SCAN: with the chain value's binade, sign
-// and mantissa (E, s, M) fixed, lane i takes block i's translation for (E, s), an exclusive
-// prefix sum over the lanes gives the mantissa block i starts from if every block before it
-// translates, and each lane tests its own block at that start. Up to the first failing block f
-// every block translates, so the prefix at f is exactly what a block-by-block walk computes; f
-// is re-run as the sequential chain and the scan resumes after it. A chunk of fast blocks costs
-// one scan instead of 64 dependent steps.
-// Re-run blocks need their (val, x) pairs, a global-memory round trip each. They are PREDICTED
-// per chunk before the walk: the same scan run with approximate continuation (after a failing
-// block f the value is taken as a + T_f, block f's chain from +0 — the true value to within its
-// rounding) names the blocks likely to fail; their staged edge values and X elements go straight
-// to LDS slots by LDS-DMA (global_load_lds_dwordx4) in one batch, so a chunk waits for memory
-// once.
-// A block that fails without having been predicted is fetched on demand into a spare slot.
 #define LGCN_EMU_CH 64
-#define LGCN_EMU_SLOTS 15   // default predicted re-run blocks per chunk with LDS slots (+1 spare)
-
-struct EmuChunk {  // one lane's share of a chunk's raw records
-    int32_t lo, hi, pk;                 // meta of block `lane`
-    float t;                            // its chain from +0 (EmuMeta::r0)
-    int32_t k[LGCN_EMU_CH / 2];         // translation (lane & 31) of block 2 j + (lane >> 5)
-};
+#define LGCN_EMU_SLOTS 12   // default LDS slots per chunk for predicted resolve blocks
+// static LDS of k_emu_walk (two 16 x 64 translation tables, 8 KB) + (2 * slots + 1) 2-KB slots
+// within a CU's 160 KB; and a chunk's slot fetches (2 per slot) + the 5 table loads after them
+// within the 62 outstanding loads wait_vm_upto waits for
+#define LGCN_EMU_MAX_SLOTS 28
 
 // Inclusive prefix sum over the 64 lanes of a wave by DPP row shifts and row broadcasts (no LDS
-// round trips: the walker's scan is on its critical path).
+// round trips: the walker's scans are on its critical path).
 __device__ __forceinline__ int wave_incl_scan(int x) {
     x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
     x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -434,56 +326,159 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
-// A block's staged edge values and X elements -> an LDS slot by LDS-DMA
-// (global_load_lds_dwordx4: the LDS destination is base + lane * 16 B; both sources are 1 KB,
-// 1 KB-aligned rows of the stage).
-__device__ __forceinline__ void fetch_block_lds(const float* __restrict__ sv,
-                                                const float* __restrict__ sx, float* v, float* xs) {
-    const int lane = threadIdx.x;
-    __builtin_amdgcn_global_load_lds(sv + 4 * lane, v, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(sx + 4 * lane, xs, 16, 0, 0);
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
-// The sequential chain over a block held in an LDS slot: a = fma(v_j, x_j, a), j < n.
-__device__ __forceinline__ float slot_chain(int n, float a, const float* __restrict__ v,
-                                            const float* __restrict__ xs) {
-    if (n == LGCN_EMU_BLOCK) {
-        // full block: the LDS reads run PF groups of 8 steps ahead of the FMAs, so only the
-        // dependent FMA chain is on the critical path
-        constexpr int NG = LGCN_EMU_BLOCK / 8, PF = 4;
-        float4 wv[PF][2], wx[PF][2];
-#pragma unroll
-        for (int g = 0; g < PF; ++g) {
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                wv[g][k] = reinterpret_cast<const float4*>(v + 8 * g)[k];
-                wx[g][k] = reinterpret_cast<const float4*>(xs + 8 * g)[k];
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const float4 cv = wv[g % PF][k], cx = wx[g % PF][k];
-                a = __builtin_fmaf(cv.x, cx.x, a);
-                a = __builtin_fmaf(cv.y, cx.y, a);
-                a = __builtin_fmaf(cv.z, cx.z, a);
-                a = __builtin_fmaf(cv.w, cx.w, a);
-            }
-            if (g + PF < NG) {
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    wv[g % PF][k] = reinterpret_cast<const float4*>(v + 8 * (g + PF))[k];
-                    wx[g % PF][k] = reinterpret_cast<const float4*>(xs + 8 * (g + PF))[k];
-                }
-            }
-            // keep the reads PF groups ahead (the scheduler would otherwise sink them next to
-            // their use and wait for each group's LDS round trip)
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return a;
+__device__ __forceinline__ uint32_t lds_byte(const void* p) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)reinterpret_cast<uintptr_t>(p));
+}
+
+// 1 KB by LDS-DMA: lane l's 16 bytes at gsrc -> LDS byte address dst + 16 l (dst wave-uniform).
+// Inline asm on purpose: a compiler-visible LDS-DMA makes the compiler drain every global load
+// in flight (vmcnt(0)) before any later LDS access of the kernel, which would serialise the
+// walker's prefetches; hidden from it, the DMA is waited for by this file's explicit vmcnt.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (at most n of this wave's vector-memory operations
+// outstanding; they complete in issue order)
+__device__ __forceinline__ void wait_vm_upto(int n) {
+    switch (n) {
+#define LGCN_WV(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        LGCN_WV(0) LGCN_WV(1) LGCN_WV(2) LGCN_WV(3) LGCN_WV(4) LGCN_WV(5) LGCN_WV(6) LGCN_WV(7)
+        LGCN_WV(8) LGCN_WV(9) LGCN_WV(10) LGCN_WV(11) LGCN_WV(12) LGCN_WV(13) LGCN_WV(14)
+        LGCN_WV(15) LGCN_WV(16) LGCN_WV(17) LGCN_WV(18) LGCN_WV(19) LGCN_WV(20) LGCN_WV(21)
+        LGCN_WV(22) LGCN_WV(23) LGCN_WV(24) LGCN_WV(25) LGCN_WV(26) LGCN_WV(27) LGCN_WV(28)
+        LGCN_WV(29) LGCN_WV(30) LGCN_WV(31) LGCN_WV(32) LGCN_WV(33) LGCN_WV(34) LGCN_WV(35)
+        LGCN_WV(36) LGCN_WV(37) LGCN_WV(38) LGCN_WV(39) LGCN_WV(40) LGCN_WV(41) LGCN_WV(42)
+        LGCN_WV(43) LGCN_WV(44) LGCN_WV(45) LGCN_WV(46) LGCN_WV(47) LGCN_WV(48) LGCN_WV(49)
+        LGCN_WV(50) LGCN_WV(51) LGCN_WV(52) LGCN_WV(53) LGCN_WV(54) LGCN_WV(55) LGCN_WV(56)
+        LGCN_WV(57) LGCN_WV(58) LGCN_WV(59) LGCN_WV(60) LGCN_WV(61) LGCN_WV(62)
+#undef LGCN_WV
+        default: break;  // >= 63: nothing to wait for
     }
-    for (int i = 0; i < n; ++i) a = __builtin_fmaf(v[i], xs[i], a);
+}
+
+// The reference's chain itself over steps [j0, j1) of a block whose (val, x) pairs lane l holds
+// for steps 4l..4l+3 (vv, xv): the value travels down the lanes — lane l applies its steps,
+// then hands the value to lane l + 1 (DPP wave_shr:1). Every lane computes with its own pairs;
+// only the lane holding the value matters, the others' results are overwritten by the shift.
+// No memory access on the chain. Returns the bits of the value after step j1 - 1.
+__device__ __forceinline__ float dpp_wave_shr1(float v) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ uint32_t seq_reg(const float (&vv)[4], const float (&xv)[4], int j0,
+                                            int j1, uint32_t a) {
+    const int lane = threadIdx.x;
+    float acc = __uint_as_float(a);
+    const int L0 = j0 >> 2, L1 = (j1 - 1) >> 2;
+    if (j0 == 0 && j1 == LGCN_EMU_BLOCK) {  // a whole block: no step masks
+        for (int L = 0; L < 64; ++L) {
+            if (L > 0) acc = dpp_wave_shr1(acc);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc = __builtin_fmaf(vv[k], xv[k], acc);
+        }
+    } else {
+        for (int L = L0; L <= L1; ++L) {
+            if (L > L0) acc = dpp_wave_shr1(acc);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 4 * lane + k;
+                const float f = __builtin_fmaf(vv[k], xv[k], acc);
+                acc = (j >= j0 && j < j1) ? f : acc;
+            }
+        }
+    }
+    return (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(acc), L1);
+}
+
+// The resolution of one block: the sequential chain a = fma(v_j, x_j, a), j < n, over the
+// block's (val, x) pairs in an LDS slot (sv, sx), read once into registers (lane l: steps
+// 4l..4l+3). With max_it = 0 (the default) it is the chain itself (seq_reg). Otherwise up to
+// max_it runs of exact integer steps first (header comment): per run, every step's q_j in the
+// chain value's binade, a wave prefix sum, and the first step that could leave the binade or be
+// a tie is taken by the reference's fma, followed by a short sequential burst; the rest of the
+// block, once the runs are spent, is the sequential chain. Measured on the Books-scale graph,
+// a chain value next to a binade boundary crosses it many times in a row (~19 exits per resolved
+// block), so the runs do not pay there; they stay as a tunable (LGCN_TUNE_EMU_RESOLVE).
+// Returns the bits of the value after the block.
+__device__ __forceinline__ uint32_t resolve_block(const float* __restrict__ sv,
+                                                  const float* __restrict__ sx, int n, uint32_t a,
+                                                  int max_it, unsigned long long* iters) {
+    constexpr int kBurst = 16;
+    const int lane = threadIdx.x;
+    const float4 v4 = *reinterpret_cast<const float4*>(sv + 4 * lane);
+    const float4 x4 = *reinterpret_cast<const float4*>(sx + 4 * lane);
+    const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+    const float xv[4] = {x4.x, x4.y, x4.z, x4.w};
+    if (max_it <= 0) return seq_reg(vv, xv, 0, n, a);
+    int le[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) le[k] = lsb_exp_prod(vv[k], xv[k]);
+    int j0 = 0;
+    for (int it = 0; j0 < n; ++it) {
+        if (it >= max_it) return seq_reg(vv, xv, j0, n, a);
+        if (iters) ++*iters;
+        const int E = (int)((a >> 23) & 255u);
+        if ((unsigned)(E - 1) >= 254u) {  // zero, subnormal, inf or NaN: the reference's steps
+            const int j1 = min(n, j0 + kBurst);
+            a = seq_reg(vv, xv, j0, j1, a);
+            j0 = j1;
+            continue;
+        }
+        const int e = E - 127;
+        const int neg = (int)(a >> 31);
+        const int M = (int)((a & 0x7fffffu) | 0x800000u);
+        const float C = __uint_as_float(((uint32_t)E << 23) | 0x400000u);  // 1.5 * 2^e
+        int q[4];
+        bool bad[4], on[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * lane + k;
+            on[k] = j >= j0 && j < n;
+            // |R - C| < 2^(e-2) keeps C + p inside binade e, so R - C = RN_u(p) exactly
+            const float R = __builtin_fmaf(vv[k], xv[k], C);
+            const float qf = ldexpf(R - C, 23 - e);
+            const bool big = !(fabsf(qf) < 2097152.f);  // >= 2^21 ulps, or NaN
+            bad[k] = on[k] && (big || le[k] >= e - 24);
+            q[k] = (on[k] && !big) ? (int)qf : 0;
+        }
+        const int c1 = q[0], c2 = c1 + q[1], c3 = c2 + q[2], c4 = c3 + q[3];
+        const int ex = wave_incl_scan(c4) - c4;
+        const int cs[4] = {ex + c1, ex + c2, ex + c3, ex + c4};  // prefix through step 4l + k
+        int fm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int mag = neg ? M - cs[k] : M + cs[k];
+            // the exact result lies within 1/2 unit of mag: inside the binade for mag in
+            // [2^23 + 1, 2^24 - 1]
+            const bool f = bad[k] || (on[k] && (mag < (1 << 23) + 1 || mag > (1 << 24) - 1));
+            fm |= f ? (1 << k) : 0;
+        }
+        const unsigned long long lanes = __ballot(fm != 0);
+        if (!lanes) {
+            const int tot = __builtin_amdgcn_readlane(cs[3], 63);
+            return a + (uint32_t)(neg ? -tot : tot);
+        }
+        const int L = (int)__builtin_ctzll(lanes);
+        const int kf = __builtin_ctz((unsigned)__builtin_amdgcn_readlane(fm, L));
+        const int f = 4 * L + kf;
+        // the steps before f translate; from step f on, a sequential burst
+        const int pbl = kf == 0 ? ex : kf == 1 ? cs[0] : kf == 2 ? cs[1] : cs[2];
+        const int pb = __builtin_amdgcn_readlane(pbl, L);
+        const int j1 = min(n, f + kBurst);
+        a = seq_reg(vv, xv, f, j1, a + (uint32_t)(neg ? -pb : pb));
+        j0 = j1;
+    }
     return a;
 }
 
@@ -491,203 +486,257 @@ template <int MODE, int XD>
 __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__ edges,
                                                  const lgcn_emu_block_t* __restrict__ blocks,
                                                  const lgcn_emu_row_t* __restrict__ rows,
-                                                 const int32_t* __restrict__ rel,
-                                                 const EmuMeta* __restrict__ meta,
+                                                 const int4* __restrict__ ktab,
+                                                 const int4* __restrict__ meta,
                                                  const float* __restrict__ stage, lgcn_rows_t x,
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
-                                                 lgcn_epilogue_t ep, int NS) {
+                                                 lgcn_epilogue_t ep, int NS, int max_it) {
     constexpr int CH = LGCN_EMU_CH;
-    constexpr int NC = LGCN_EMU_CANDS;
+    constexpr int B = LGCN_EMU_BLOCK;
     static_assert(CH == 64, "one lane per block of a chunk");
-    __shared__ int32_t s_k[CH * NC], s_min[CH * NC], s_max[CH * NC];
-    __shared__ float2 sq[LGCN_EMU_BLOCK];            // no-stage mode: gathered (val, x)
-    // NS + 1 slots (dynamic LDS, sized at launch): re-run blocks' edge values, then their X
-    // elements. Fewer slots = less LDS per wave = more walk waves per CU (short-row parts).
+    // translation tables of two chunks, [binade][block]: lane reads are conflict-free
+    __shared__ int32_t sK[2][kNB][CH];
+    // 2 sets x NS slots (chunk c uses set c & 1) + one spare: a block's edge values, then its
+    // X elements (dynamic LDS, sized at launch)
     extern __shared__ __attribute__((aligned(16))) float s_dyn[];
-    auto s_v = [&](int sl) { return s_dyn + sl * LGCN_EMU_BLOCK; };
-    auto s_xs = [&](int sl) { return s_dyn + (NS + 1 + sl) * LGCN_EMU_BLOCK; };
+    auto slot_v = [&](int i) { return s_dyn + i * 2 * B; };
+    auto slot_x = [&](int i) { return s_dyn + i * 2 * B + B; };
     const int lane = threadIdx.x;
     const int c = blockIdx.y;
     const lgcn_emu_row_t er = rows[blockIdx.x];
-    // the chain value, as its bits (wave-uniform)
-    uint32_t ab = __float_as_uint(meta[(int64_t)er.first_block * d + c].r0);
-    auto stage_of = [&](int64_t bi) -> const float* {
-        return stage ? stage + (bi * (d + 1) + c) * LGCN_EMU_BLOCK : nullptr;
-    };
-    auto load_chunk = [&](int32_t b0, EmuChunk& ck) {
-        const int nb = min(CH, er.n_blocks - b0);
-        const int64_t bl = er.first_block + b0 + min(lane, max(nb - 1, 0));
-        const int4 mv = *reinterpret_cast<const int4*>(meta + bl * d + c);
-        ck.lo = mv.x;
-        ck.hi = mv.y;
-        ck.pk = lane < nb ? mv.z : (int)0x80000000;  // past the row: identity
-        ck.t = __int_as_float(mv.w);
-        const int64_t base = (int64_t)(er.first_block + b0) * d + c;
-#pragma unroll
-        for (int j = 0; j < CH / 2; ++j) {
-            const int bb = min(2 * j + (lane >> 5), max(nb - 1, 0));
-            ck.k[j] = rel[(base + (int64_t)bb * d) * NC + (lane & 31)];
-        }
-    };
-    // chunk -> LDS: translations and, per (block, candidate k = 2 w + sign), the valid range of
-    // the start mantissa M (empty when the candidate's own chain may have left its binade)
-    auto stage_chunk = [&](const EmuChunk& ck) {
-        constexpr int LB = (1 << 23) + kSlack, HB = (1 << 24) - kSlack, C = 3 << 22;
-        const int k = lane & 31;
-        const int w = k >> 1;
-        const bool neg = k & 1;
-#pragma unroll
-        for (int j = 0; j < CH / 2; ++j) {
-            const int b = 2 * j + (lane >> 5);
-            const int32_t lo0 = __shfl(ck.lo, b);
-            const int32_t hi0 = __shfl(ck.hi, b);
-            const int lo = lo0 >> w, hi = -((-hi0) >> w);
-            const int mlo = neg ? -hi : lo, mhi = neg ? -lo : hi;  // magnitude offsets
-            const bool valid = C + mlo >= LB && C + mhi <= HB;
-            s_k[b * NC + k] = ck.k[j];
-            s_min[b * NC + k] = valid ? LB - mlo : 1 << 24;
-            s_max[b * NC + k] = valid ? HB - mhi : 0;
-        }
-    };
-    // block k of the row holds edges [row_beg + k * BLOCK, min(.. + BLOCK, row_end)) (plan_emulation)
-    const int32_t row_beg = blocks[er.first_block].beg;
-    const int32_t row_end = blocks[er.first_block + er.n_blocks - 1].end;
-    auto fetch_slot = [&](int32_t kb, int s) {
-        const int64_t bi = er.first_block + kb;
-        fetch_block_lds(stage + (bi * (d + 1) + d) * LGCN_EMU_BLOCK, stage_of(bi), s_v(s),
-                        s_xs(s));
-    };
+    const int64_t fb = er.first_block;
+    const int nb_all = er.n_blocks;
+    // block k of the row holds edges [row_beg + k * B, min(.. + B, row_end)) (plan_emulation)
+    const int32_t row_beg = blocks[fb].beg;
+    const int32_t row_end = blocks[fb + nb_all - 1].end;
+    // the chain value as its bits (wave-uniform); block 0's chain from +0 is the true chain
+    uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(meta[fb * d + c].w);
+    const int nch = (nb_all - 1 + CH - 1) / CH;  // chunks of blocks 1, 2, ...
+    const bool staged = stage != nullptr;
+    const int spare = 2 * NS;
 #ifdef LGCN_EMU_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long n_fast = 0, n_slow = 0, t_slow = 0;
+    unsigned long long n_fast = 0, n_slow = 0, t_slow = 0, n_iter = 0;
     unsigned long long ph[16] = {0};
     unsigned long long ph_last = t_start;
+    unsigned long long* iters = &n_iter;
+#else
+    unsigned long long* iters = nullptr;
 #endif
-    EmuChunk nxt;
-    if (er.n_blocks > 1) load_chunk(1, nxt);
-    for (int32_t b0 = 1; b0 < er.n_blocks; b0 += CH) {
-        const int nb = min(CH, er.n_blocks - b0);
-        wave_lds_sync();  // the previous chunk's LDS rows and slots are no longer read
-        stage_chunk(nxt);
-        const int my_eb = (int)(int16_t)(nxt.pk & 0xffff);   // lane i: block i's ebase,
-        const int my_ml = (int)(int16_t)(nxt.pk >> 16);      // maxlsb,
-        const float my_t = nxt.t;                            // and chain from +0
-        const bool my_id = my_ml == kIdentity;  // every product zero: translation by 0
-        wave_lds_sync();
-        PH_MARK(0);
-        PH_COUNT(8, 1);
-        // The speculative test from block `from` with chain value bits `a`: lane i's start
-        // mantissa if every block in [from, i) translates (exclusive prefix of the mantissa
-        // changes), and the mask of blocks that cannot translate from there. `incl` returns the
-        // inclusive prefix, `dm` the lane's own change.
-        auto test = [&](uint32_t a, int from, int& incl, int& dm) -> unsigned long long {
-            const int E = (int)((a >> 23) & 255u);
-            const int neg = (int)(a >> 31);
-            const int M = (int)((a & 0x7fffffu) | 0x800000u);
-            const int w = E - 127 - my_eb;
-            const int idx = lane * NC + 2 * min(max(w, 0), kW - 1) + neg;
-            const int32_t K = s_k[idx], mn = s_min[idx], mx = s_max[idx];
-            const bool act = lane < nb && lane >= from;
-            dm = act && !my_id ? (neg ? -K : K) : 0;  // |K| < 2^24: the sums fit in int32
-            incl = wave_incl_scan(dm);
-            const int start = M + incl - dm;
-            bool ok = my_id || (((unsigned)(E - 1) < 254u) & ((unsigned)w < (unsigned)kW) &
-                                (my_ml < E - 127 - 24) & (start >= mn) & (start <= mx));
-            LGCN_EMU_FORCE(ok);
-            return __ballot(act && !ok);
-        };
-        // predicted re-run blocks of this chunk (stage mode: their data goes to LDS slots)
-        unsigned long long pred = 0;
-        if (stage) {
-            uint32_t pa = ab;
-            int from = 0;
-            for (int it = 0; it < NS && from < nb; ++it) {
-                int incl, dm;
-                const unsigned long long bad = test(pa, from, incl, dm);
-                if (!bad) break;
-                const int f = (int)__builtin_ctzll(bad);
+    struct Tab {
+        int4 m;
+        int4 k[4];
+    };
+    auto chunk_nb = [&](int ch) { return min(CH, nb_all - 1 - ch * CH); };
+    auto load_tab = [&](int ch, Tab& t) {  // 5 loads per lane (lane = block)
+        const int nb = chunk_nb(ch);
+        const int64_t rc = (fb + 1 + (int64_t)ch * CH + min(lane, nb - 1)) * d + c;
+        t.m = meta[rc];
+        const int4* kp = ktab + rc * 4;
+        t.k[0] = kp[0];
+        t.k[1] = kp[1];
+        t.k[2] = kp[2];
+        t.k[3] = kp[3];
+    };
+    auto stage_tab = [&](const Tab& t, int buf) {
+        const int kk[kNB] = {t.k[0].x, t.k[0].y, t.k[0].z, t.k[0].w, t.k[1].x, t.k[1].y,
+                             t.k[1].z, t.k[1].w, t.k[2].x, t.k[2].y, t.k[2].z, t.k[2].w,
+                             t.k[3].x, t.k[3].y, t.k[3].z, t.k[3].w};
+#pragma unroll
+        for (int w = 0; w < kNB; ++w) sK[buf][w][lane] = kk[w];
+    };
+    // The speculative test of chunk blocks [from, nb) from chain value bits a, with table `buf`
+    // and the lane's block meta m: lane i's start mantissa if every block in [from, i)
+    // translates (exclusive prefix of the magnitude changes), and the ballot of the blocks that
+    // cannot translate from there. `incl` returns the inclusive prefix, `dm` the lane's change.
+    // margin: the prediction widens the bounds (its start value is approximate).
+    auto test = [&](uint32_t a, int from, int nb, int buf, const int4& m, bool margin, int& incl,
+                    int& dm) -> unsigned long long {
+        const int E = (int)((a >> 23) & 255u);
+        const int neg = (int)(a >> 31);
+        const int M = (int)((a & 0x7fffffu) | 0x800000u);
+        const int eb = (int)(int16_t)(m.z & 0xffff);
+        const uint32_t vm = (uint32_t)m.z >> 16;
+        const bool ident = eb == kIdentEb;
+        const int w = E - 127 - eb;
+        const bool inw = ((unsigned)(E - 1) < 254u) && ((unsigned)w < (unsigned)kNB) &&
+                         ((vm >> (w & (kNB - 1))) & 1u);
+        const int wc = inw ? w : 0;
+        const int K = sK[buf][wc][lane];
+        const int lo = m.x >> wc, hi = -((-m.y) >> wc);
+        const bool act = lane >= from && lane < nb;
+        dm = (act && inw && !ident) ? (neg ? -K : K) : 0;  // |K| < 2^24: the sums fit in int32
+        incl = wave_incl_scan(dm);
+        const int start = M + incl - dm;
+        const int alo = neg ? -hi : lo, ahi = neg ? -lo : hi;
+        const int mg = margin ? ((hi - lo) >> 4) + 64 : 0;
+        bool ok = ident || (inw && start + alo >= kLB + mg && start + ahi <= kHB - mg);
+        LGCN_EMU_FORCE(ok);
+        return __ballot(act && !ok);
+    };
+    // Chunk ch's blocks predicted to need a resolve from the approximate start bits pa (after a
+    // failing block f the value continues as a + r0_f, block f's chain from +0 — the true value
+    // to within its rounding); at most NS are recorded. Returns the approximate end value.
+    auto predict = [&](int ch, int buf, const int4& m, uint32_t pa,
+                       unsigned long long& pred) -> uint32_t {
+        const int nb = chunk_nb(ch);
+        pred = 0;
+        int from = 0, np = 0;
+        for (int it = 0; from < nb; ++it) {
+            int incl, dm;
+            const unsigned long long bad = test(pa, from, nb, buf, m, true, incl, dm);
+            if (!bad) return pa + (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+            const int f = (int)__builtin_ctzll(bad);
+            if (np < NS) {
                 pred |= 1ull << f;
-                pa += (uint32_t)__builtin_amdgcn_readlane(incl - dm, f);
-                pa = __float_as_uint(__uint_as_float(pa) + __int_as_float(
-                         __builtin_amdgcn_readlane(__float_as_int(my_t), f)));
-                from = f + 1;
+                ++np;
+            }
+            pa += (uint32_t)__builtin_amdgcn_readlane(incl - dm, f);
+            pa = __float_as_uint(__uint_as_float(pa) +
+                                 __int_as_float(__builtin_amdgcn_readlane(m.w, f)));
+            pa = (uint32_t)__builtin_amdgcn_readfirstlane((int)pa);
+            from = f + 1;
+            if (it >= NS + 32) {  // the rest approximated by their chains from +0
+                const float s = wave_sum_f((lane >= from && lane < nb) ? __int_as_float(m.w)
+                                                                       : 0.f);
+                return (uint32_t)__builtin_amdgcn_readfirstlane(
+                    (int)__float_as_uint(__uint_as_float(pa) + s));
             }
         }
-        PH_MARK(1);
-        PH_COUNT(9, __builtin_popcountll(pred));
-        if (b0 + CH < er.n_blocks) load_chunk(b0 + CH, nxt);  // in flight during this chunk
-        if (pred) {
-            int s = 0;
-            for (unsigned long long m = pred; m; m &= m - 1, ++s)
-                fetch_slot(b0 + (int)__builtin_ctzll(m), s);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slots (and the next chunk) landed
+        return pa;
+    };
+    auto fetch = [&](int64_t bi, int slot) {  // block bi's staged values -> LDS slot (2 DMAs)
+        dma16(stage + (bi * (d + 1) + d) * B + 4 * lane, lds_byte(slot_v(slot)));
+        dma16(stage + (bi * (d + 1) + c) * B + 4 * lane, lds_byte(slot_x(slot)));
+    };
+    auto issue_slots = [&](int ch, unsigned long long pred, int set) {
+        int s = 0;
+        for (unsigned long long m = pred; m; m &= m - 1, ++s)
+            fetch(fb + 1 + (int64_t)ch * CH + __builtin_ctzll(m), set * NS + s);
+    };
+    if (nch > 0) {
+        Tab tn;
+        int4 mc, mn = make_int4(0, 0, 0, 0);
+        load_tab(0, tn);
+        stage_tab(tn, 0);
+        mc = tn.m;
+        unsigned long long pred_c = 0, pred_n = 0;
+        uint32_t start_c = ab;                     // assumed start of chunk ch's prediction
+        uint32_t end_c = predict(0, 0, mc, ab, pred_c);  // and its predicted end
+        if (!staged) pred_c = 0;
+        issue_slots(0, pred_c, 0);
+        if (nch > 1) {
+            load_tab(1, tn);
+            stage_tab(tn, 1);
+            mn = tn.m;
         }
-        PH_MARK(2);
-        // lane i: the slot holding block i's data, or -1
-        const int my_slot = ((pred >> lane) & 1ull)
-            ? (int)__builtin_popcountll(pred & ((1ull << lane) - 1ull)) : -1;
-        int from = 0;
-        while (true) {
-            int incl, dm;
-            const unsigned long long bad = test(ab, from, incl, dm);
-            const int f = bad ? (int)__builtin_ctzll(bad) : nb;
-            // blocks [from, f) translate: their mantissa changes add to the bits (same binade)
-            ab += (uint32_t)(f < nb ? __builtin_amdgcn_readlane(incl - dm, f)
-                                    : __builtin_amdgcn_readlane(incl, 63));
-            PH_MARK(3);
-            EMU_STAT(0, f - from);
+        if (nch > 2) load_tab(2, tn);  // in flight during chunk 0
+        PH_MARK(0);
+        for (int ch = 0; ch < nch; ++ch) {
+            const int buf = ch & 1;
+            const int nb = chunk_nb(ch);
+            // prediction of chunk ch + 1 (its start: chunk ch's predicted end, moved by the
+            // error of chunk ch's assumed start) and its slot fetches, in flight during ch
+            int after = ch + 2 < nch ? 5 : 0;  // loads issued after chunk ch's slots: table ch+2
+            uint32_t start_n = 0, end_n = 0;
+            if (ch + 1 < nch) {
+                start_n = __float_as_uint(__uint_as_float(end_c) +
+                                          (__uint_as_float(ab) - __uint_as_float(start_c)));
+                start_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)start_n);
+                end_n = predict(ch + 1, buf ^ 1, mn, start_n, pred_n);
+                if (!staged) pred_n = 0;
+                issue_slots(ch + 1, pred_n, buf ^ 1);
+                after += 2 * __builtin_popcountll(pred_n);
+            }
+            PH_MARK(1);
+            PH_COUNT(8, 1);
+            PH_COUNT(9, __builtin_popcountll(pred_c));
+            wait_vm_upto(after);  // chunk ch's slots have landed
+            PH_MARK(2);
+            int from = 0;
+            while (true) {
+                int incl, dm;
+                const unsigned long long bad = test(ab, from, nb, buf, mc, false, incl, dm);
+                const int f = bad ? (int)__builtin_ctzll(bad) : nb;
+                // blocks [from, f) translate: their mantissa changes add to the bits
+                const int tv = f < nb ? incl - dm : incl;
+                ab += (uint32_t)__builtin_amdgcn_readlane(tv, f < nb ? f : 63);
+                PH_MARK(3);
+                EMU_STAT(0, f - from);
 #ifdef LGCN_EMU_STATS
-            n_fast += f - from;
+                n_fast += f - from;
 #endif
-            if (f >= nb) break;
-            // re-run block f as the reference does
-            const int32_t kb = b0 + f;
-            const int32_t f_beg = row_beg + kb * LGCN_EMU_BLOCK;
-            const int32_t n = min(f_beg + LGCN_EMU_BLOCK, row_end) - f_beg;
-            EMU_STAT(1, 1);
-            EMU_STAT(7, n);
+                if (f >= nb) break;
+                const int kb = 1 + ch * CH + f;  // block index in the row
+                const int32_t bbeg = row_beg + kb * B;
+                const int n = min(bbeg + B, row_end) - bbeg;
+                EMU_STAT(1, 1);
 #ifdef LGCN_EMU_STATS
-            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-            EMU_STAT(2, __builtin_amdgcn_readlane(my_slot, f) < 0);  // not predicted
+                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-            float a;
-            if (stage) {
-                int sl = __builtin_amdgcn_readlane(my_slot, f);
-                if (sl < 0) {  // not predicted: fetch now into the spare slot
-                    sl = NS;
-                    wave_lds_sync();
-                    fetch_slot(kb, sl);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    PH_MARK(5);
+                int sl;
+                if ((pred_c >> f) & 1ull) {
+                    sl = buf * NS + __builtin_popcountll(pred_c & ((1ull << f) - 1ull));
+                } else {  // not predicted: fetched now into the spare slot
+                    sl = spare;
+                    EMU_STAT(3, 1);
                     PH_COUNT(11, 1);
+                    if (staged) {
+                        fetch(fb + kb, sl);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    } else {
+                        // no stage: the block's edge records and X elements, gathered
+                        float vq[4], xq[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int j = 4 * lane + k;
+                            const int2 r = *reinterpret_cast<const int2*>(
+                                edges + bbeg + min(j, n - 1));
+                            vq[k] = j < n ? __int_as_float(r.y) : 0.f;
+                            xq[k] = load_elem<XD>(x, x_nz, r.x, c, xdiv, j < n);
+                        }
+                        *reinterpret_cast<float4*>(slot_v(sl) + 4 * lane) =
+                            make_float4(vq[0], vq[1], vq[2], vq[3]);
+                        *reinterpret_cast<float4*>(slot_x(sl) + 4 * lane) =
+                            make_float4(xq[0], xq[1], xq[2], xq[3]);
+                    }
+                    PH_MARK(5);
                 }
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
-                a = g_emu_mode == 1 ? __uint_as_float(ab)
-                                    : slot_chain(n, __uint_as_float(ab), s_v(sl), s_xs(sl));
-#else
-                a = slot_chain(n, __uint_as_float(ab), s_v(sl), s_xs(sl));
+                if (g_emu_mode != 1)
 #endif
-            } else {
-                SlowData sd;
-                slow_load<XD>(sd, edges, f_beg, f_beg + n, x, xdiv, x_nz, nullptr, c);
-                slow_stage(sd, n, false, sq);
-                a = slow_chain(n, __uint_as_float(ab), sq);
-            }
-            ab = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(a));
-            PH_MARK(4);
-            PH_COUNT(10, 1);
+                    ab = resolve_block(slot_v(sl), slot_x(sl), n, ab, max_it, iters);
+                PH_MARK(4);
+                PH_COUNT(10, 1);
 #ifdef LGCN_EMU_STATS
-            ++n_slow;
-            t_slow += __builtin_amdgcn_s_memtime() - t0;
+                ++n_slow;
+                t_slow += __builtin_amdgcn_s_memtime() - t0;
 #endif
-            from = f + 1;
-            if (from >= nb) break;
+                from = f + 1;
+                if (from >= nb) break;
+            }
+            // rotate: chunk ch + 2's table into chunk ch's buffer, chunk ch + 3's loads
+            if (ch + 2 < nch) {
+                stage_tab(tn, buf);
+                mc = mn;
+                mn = tn.m;
+            } else {
+                mc = mn;
+            }
+            if (ch + 3 < nch) load_tab(ch + 3, tn);
+            PH_MARK(0);
+            pred_c = pred_n;
+            start_c = start_n;
+            end_c = end_n;
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA lands after the wave is gone
 #ifdef LGCN_EMU_STATS
+    ph[12] = n_iter;
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
         for (int k = 0; k < 16; ++k) g_emu_phase[k] += ph[k];
+    if (lane == 0) atomicAdd(&g_emu_stats[4], n_iter);
     if (lane == 0 && blockIdx.x < 256) {
         atomicAdd(&g_emu_row_stats[blockIdx.x][0], n_fast);
         atomicAdd(&g_emu_row_stats[blockIdx.x][1], n_slow);
@@ -722,23 +771,29 @@ bool is_pow2(float x) {
 
 template <int XD>
 int launch_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
-                  const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, int32_t* rel,
-                  EmuMeta* meta, float* stage, hipStream_t s) {
+                  const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, int4* ktab,
+                  int4* meta, float* stage, hipStream_t s) {
     const dim3 grid((uint32_t)n_blocks, (uint32_t)((d + 63) / 64));
     hipLaunchKernelGGL((k_emu_blocks<XD>), grid, dim3(64), 0, s, edges, blocks, x, xdiv, x_nz, d,
-                       rel, meta, stage);
+                       ktab, meta, stage);
     return herr_x(hipGetLastError());
 }
 
 template <int MODE, int XD>
 int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                const lgcn_emu_row_t* rows, int32_t n_rows, const int32_t* rel, const EmuMeta* meta,
+                const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
                 const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
                 int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
     const dim3 grid((uint32_t)n_rows, (uint32_t)d);
-    const size_t lds = (size_t)2 * (slots + 1) * LGCN_EMU_BLOCK * sizeof(float);
-    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, rel,
-                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots);
+    const size_t lds = (size_t)(2 * slots + 1) * 2 * LGCN_EMU_BLOCK * sizeof(float);
+    if (lds > 56 * 1024) {  // beyond the default dynamic-LDS limit: raise it once per kernel
+        static const hipError_t once = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&k_emu_walk<MODE, XD>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
+        if (once != hipSuccess) return (int)once;
+    }
+    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, ktab,
+                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots, lgcn_detail::g_emu_resolve);
     return herr_x(hipGetLastError());
 }
 
@@ -748,18 +803,17 @@ int xd_of(float xdiv, const uint32_t* x_nz) {
 
 template <int MODE>
 int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-              const lgcn_emu_row_t* rows, int32_t n_rows, const int32_t* rel, const EmuMeta* meta,
+              const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
               const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
               int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
 #define LGCN_W(XD_) \
-    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, rel, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, s);
+    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, s);
     switch (xd) {
         LGCN_W(0) LGCN_W(1) LGCN_W(2) LGCN_W(4) LGCN_W(5) LGCN_W(6)
         default: return LGCN_EINVAL;
     }
 #undef LGCN_W
 }
-
 
 // ---------------------------------------------------------------------------------------------
 // mid-size hub rows: the reference's sequential chain itself, latency-hidden
@@ -785,35 +839,13 @@ struct ChainCfg {
     static constexpr int NR = 2 * AHEAD + 1;  // record windows in the ring
 };
 
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)reinterpret_cast<uintptr_t>(p);
-}
-
-// 16 LDS reads at a + OFF + t * STRIDE, completed before the values are used. Inline asm on
-// purpose: LDS written by LDS-DMA makes the compiler wait for EVERY outstanding global load
-// before any compiler-visible LDS read (it cannot tell the ring slots apart), which would drain
-// the gathers in flight; here the waits are explicit (vmcnt before, lgkmcnt inside).
-template <int OFF, int STRIDE>
-__device__ __forceinline__ void lds_read16(uint32_t a, float (&v)[16]) {
-    asm volatile(
-        "ds_read_b32 %0, %16 offset:%17\n\tds_read_b32 %1, %16 offset:%18\n\t"
-        "ds_read_b32 %2, %16 offset:%19\n\tds_read_b32 %3, %16 offset:%20\n\t"
-        "ds_read_b32 %4, %16 offset:%21\n\tds_read_b32 %5, %16 offset:%22\n\t"
-        "ds_read_b32 %6, %16 offset:%23\n\tds_read_b32 %7, %16 offset:%24\n\t"
-        "ds_read_b32 %8, %16 offset:%25\n\tds_read_b32 %9, %16 offset:%26\n\t"
-        "ds_read_b32 %10, %16 offset:%27\n\tds_read_b32 %11, %16 offset:%28\n\t"
-        "ds_read_b32 %12, %16 offset:%29\n\tds_read_b32 %13, %16 offset:%30\n\t"
-        "ds_read_b32 %14, %16 offset:%31\n\tds_read_b32 %15, %16 offset:%32\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
-          "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
-          "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
-        : "v"(a), "n"(OFF), "n"(OFF + STRIDE), "n"(OFF + 2 * STRIDE), "n"(OFF + 3 * STRIDE),
-          "n"(OFF + 4 * STRIDE), "n"(OFF + 5 * STRIDE), "n"(OFF + 6 * STRIDE),
-          "n"(OFF + 7 * STRIDE), "n"(OFF + 8 * STRIDE), "n"(OFF + 9 * STRIDE),
-          "n"(OFF + 10 * STRIDE), "n"(OFF + 11 * STRIDE), "n"(OFF + 12 * STRIDE),
-          "n"(OFF + 13 * STRIDE), "n"(OFF + 14 * STRIDE), "n"(OFF + 15 * STRIDE)
-        : "memory");
+// 4 bytes per lane by LDS-DMA: lane l's dword at gsrc -> LDS byte address dst + 4 l (dst
+// wave-uniform); hidden from the compiler like dma16.
+__device__ __forceinline__ void dma4(const void* gsrc, uint32_t dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
 }
 
 template <int N>
@@ -848,28 +880,29 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     const int64_t dl = 2 * (int64_t)end - 1, dlast = 2 * (int64_t)end - 2 + (lane & 1);
     auto rec_dma = [&](int32_t w) {
         const int64_t d0 = 2 * ((int64_t)beg + 64 * w) + lane;
-        int32_t* dst = reinterpret_cast<int32_t*>(&s_rec[w % NR][0]);
-        __builtin_amdgcn_global_load_lds(ew + (d0 <= dl ? d0 : dlast), dst, 4, 0, 0);
-        __builtin_amdgcn_global_load_lds(ew + (d0 + 64 <= dl ? d0 + 64 : dlast), dst + 64, 4, 0, 0);
+        const uint32_t dst = lds_byte(&s_rec[w % NR][0]);
+        dma4(ew + (d0 <= dl ? d0 : dlast), dst);
+        dma4(ew + (d0 + 64 <= dl ? d0 + 64 : dlast), dst + 256);
     };
     // gathered X of window w -> s_x[w % NX]: instruction k moves rows k*RPI .. k*RPI + RPI - 1
     // (lane -> row sub = lane / LPR, 16-B piece q = lane % LPR); the columns come from LDS
     const int sub = lane / C::LPR, q = lane % C::LPR;
     auto x_dma = [&](int32_t w) {
-        float cols[16];
-        lds_read16<0, C::RPI * 8>(lds_addr(&s_rec[w % NR][sub]), cols);
-        float* dst = s_x[w % NX];
+        int32_t cols[C::NI];
 #pragma unroll
-        for (int k = 0; k < C::NI; ++k) {
-            const float* src = seg_row_sel(x, __float_as_int(cols[k])) + c0 + 4 * q;
-            __builtin_amdgcn_global_load_lds(src, dst + k * 256, 16, 0, 0);
-        }
+        for (int k = 0; k < C::NI; ++k) cols[k] = s_rec[w % NR][k * C::RPI + sub].x;
+        const uint32_t dst = lds_byte(s_x[w % NX]);
+#pragma unroll
+        for (int k = 0; k < C::NI; ++k)
+            dma16(seg_row_sel(x, cols[k]) + c0 + 4 * q, dst + k * 1024);
     };
     // Pipeline (A = AHEAD): iteration v issues x(v + A) then rec(v + 2A); the prologue runs
     // v = -A .. -1 after rec(0 .. A-1) have landed. At iteration w, x(w) and rec(w + A) (both
     // issued by iteration w - A) must have landed: A - 1 later iterations of NI + 2 loads each
     // may still be in flight. Ring slots: x(w + A) reuses window w - 1's slot (NX = A + 1),
-    // rec(w + 2A) record window w - 1's (NR = 2A + 1).
+    // rec(w + 2A) record window w - 1's (NR = 2A + 1). The LDS-DMA is hidden from the compiler
+    // (dma4 / dma16): its LDS reads are then ordinary, scheduled and counted by it, and the
+    // explicit vmcnt waits (asm, "memory") keep them behind the data they read.
     static_assert(NX == AHEAD + 1 && NR == 2 * AHEAD + 1, "ring sizes");
     for (int w = 0; w < AHEAD; ++w) rec_dma(w);
     wait_vm<0>();
@@ -884,35 +917,46 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
         x_dma(w + AHEAD);
         rec_dma(w + 2 * AHEAD);
         const int n = min(64, end - beg - 64 * w);
-        const uint32_t xa = lds_addr(&s_x[w % NX][cc]);
-        const uint32_t va = lds_addr(&s_rec[w % NR][0].y);  // same address in every lane
-        // 16 steps at a time: X elements and (broadcast) edge values from LDS, then the chain;
-        // only the row's last window is partial (steps past n leave acc alone)
-#define LGCN_CHAIN_FOLD(G, FULL)                                                              \
-        {                                                                                     \
-            float xv[16], vv[16];                                                             \
-            lds_read16<(G) * W * 4, W * 4>(xa, xv);                                           \
-            lds_read16<(G) * 8, 8>(va, vv);                                                   \
-            _Pragma("unroll") for (int t = 0; t < 16; ++t) {                                  \
-                float xe = xv[t];                                                             \
-                if constexpr ((XD & 3) == 1) xe = xe / xdiv;                                  \
-                else if constexpr ((XD & 3) == 2) xe = xe * xdiv;                             \
-                if (FULL) acc = __builtin_fmaf(vv[t], xe, acc);                               \
-                else acc = (G) + t < n ? __builtin_fmaf(vv[t], xe, acc) : acc;                \
-            }                                                                                 \
-        }
+        const float* xs = &s_x[w % NX][cc];  // step j's element of column cc: xs[j * W]
+        // lane l holds step l's edge value; a step reads it by v_readlane (a scalar operand)
+        const float vw = __int_as_float(s_rec[w % NR][lane].y);
+        // groups of 8 steps: group g + 1's LDS reads are issued before group g is folded (the
+        // sched_barriers keep the compiler from sinking them next to their use)
+        float xg[2][8];
+        auto load8 = [&](float (&r)[8], int g) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) r[t] = xs[(8 * g + t) * W];
+        };
+        auto fold8 = [&](const float (&r)[8], int g, bool full) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                float xe = r[t];
+                if constexpr ((XD & 3) == 1) xe = xe / xdiv;
+                else if constexpr ((XD & 3) == 2) xe = xe * xdiv;
+                const int j = 8 * g + t;
+                const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vw), j));
+                const float f = __builtin_fmaf(v, xe, acc);
+                acc = (full || j < n) ? f : acc;
+            }
+        };
+        load8(xg[0], 0);
         if (n == 64) {
-            LGCN_CHAIN_FOLD(0, true)
-            LGCN_CHAIN_FOLD(16, true)
-            LGCN_CHAIN_FOLD(32, true)
-            LGCN_CHAIN_FOLD(48, true)
-        } else {
-            LGCN_CHAIN_FOLD(0, false)
-            LGCN_CHAIN_FOLD(16, false)
-            LGCN_CHAIN_FOLD(32, false)
-            LGCN_CHAIN_FOLD(48, false)
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                if (g + 1 < 8) load8(xg[(g + 1) & 1], g + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                fold8(xg[g & 1], g, true);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {  // the row's last window: steps past n leave acc alone
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                if (g + 1 < 8) load8(xg[(g + 1) & 1], g + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                fold8(xg[g & 1], g, false);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
-#undef LGCN_CHAIN_FOLD
     }
     wait_vm<0>();  // no LDS-DMA may land after the wave (and its LDS) is gone
     if (lane >= W || c0 + lane >= d) return;
@@ -1004,13 +1048,16 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
     if (n_blocks < 0 || d < 1 || d > 2048 || !(x_div > 0.f)) return LGCN_EINVAL;
     if (n_blocks == 0) return 0;
     if (!edges || !blocks || !rel || !meta || !x.p0) return LGCN_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(rel) & 15) || (reinterpret_cast<uintptr_t>(meta) & 15) ||
+        (reinterpret_cast<uintptr_t>(stage) & 15))
+        return LGCN_EALIGN;
     const int xd = xd_of(x_div, x_nz);
     const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    EmuMeta* mp = static_cast<EmuMeta*>(meta);
-    int32_t* rp = reinterpret_cast<int32_t*>(rel);
+    int4* mp = static_cast<int4*>(meta);
+    int4* kp = reinterpret_cast<int4*>(rel);
 #define LGCN_B(XD_) \
-    case XD_: return launch_blocks<XD_>(edges, blocks, n_blocks, x, xa, x_nz, d, rp, mp, stage, s);
+    case XD_: return launch_blocks<XD_>(edges, blocks, n_blocks, x, xa, x_nz, d, kp, mp, stage, s);
     switch (xd) {
         LGCN_B(0) LGCN_B(1) LGCN_B(2) LGCN_B(4) LGCN_B(5) LGCN_B(6)
         default: return LGCN_EINVAL;
@@ -1024,11 +1071,15 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
                   void* stream) {
     if (slots == 0) slots = LGCN_EMU_SLOTS;
+    // static LDS (two translation tables, 8 KB) + (2 slots + 1) x 2 KB within 64 KB
     if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host || slots < 1 ||
-        slots > 63)
+        slots > LGCN_EMU_MAX_SLOTS)
         return LGCN_EINVAL;
     if (n_rows == 0) return 0;
     if (!edges || !blocks || !rows || !rel || !meta || !y || ldy < d || !x.p0) return LGCN_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(rel) & 15) || (reinterpret_cast<uintptr_t>(meta) & 15) ||
+        (reinterpret_cast<uintptr_t>(stage) & 15))
+        return LGCN_EALIGN;
     lgcn_epilogue_t ep = *epi_host;
     if (ep.mode == LGCN_EPI_MEAN && (ep.n_prev < 1 || ep.n_prev - 1 > LGCN_MAX_LAYERS))
         return LGCN_EINVAL;
@@ -1044,15 +1095,15 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     const int xd = xd_of(x_div, x_nz);
     const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const EmuMeta* mp = static_cast<const EmuMeta*>(meta);
-    const int32_t* rl = reinterpret_cast<const int32_t*>(rel);
+    const int4* mp = static_cast<const int4*>(meta);
+    const int4* kp = reinterpret_cast<const int4*>(rel);
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
+            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         case LGCN_EPI_MEAN:
-            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
+            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         case LGCN_EPI_ADD:
-            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, rl, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
+            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
         default:
             return LGCN_EINVAL;
     }

@@ -24,8 +24,9 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
-ABI_VERSION = 7
-LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 32, 16, 256
+TUNE_EMU_RESOLVE = 5
+ABI_VERSION = 8
+LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
 # bitwise = reference CPU path). Longer rows ("hubs") follow the hub mode:
@@ -172,6 +173,9 @@ def load_library(path=None):
         # LGCN_MEAN_PREFETCH=off: A/B switch of the MEAN layer's bundle prefetch (same bits)
         if os.environ.get("LGCN_MEAN_PREFETCH", "").lower() in ("0", "off"):
             lib.lgcn_tune(TUNE_MEAN_PREFETCH, 2)
+        # LGCN_EMU_RESOLVE=k: A/B switch of the walk's parallel runs per resolved block (same bits)
+        if os.environ.get("LGCN_EMU_RESOLVE", ""):
+            lib.lgcn_tune(TUNE_EMU_RESOLVE, int(os.environ["LGCN_EMU_RESOLVE"]))
         _lib = lib
         return lib
 
@@ -273,7 +277,8 @@ class HubPlan:
     epilogue in place) and rows above emu_min are emulated (`emu_blocks` / `emu_rows`)."""
 
     def __init__(self, threshold, mode="exact", chunk=None, items=None, rows=None, n_slots=0,
-                 n_hub_rows=0, n_pre=0, emu_blocks=None, emu_rows=None, emu_min=None):
+                 n_hub_rows=0, n_pre=0, emu_blocks=None, emu_rows=None, emu_min=None,
+                 emu_nb=None):
         self.threshold = threshold
         self.mode = mode
         self.chunk = chunk
@@ -289,6 +294,8 @@ class HubPlan:
         self.emu_rows = emu_rows      # int32 [n_emu_rows, 4] (lgcn_emu_row_t)
         self.n_emu_blocks = 0 if emu_blocks is None else emu_blocks.shape[0]
         self.n_emu_rows = 0 if emu_rows is None else emu_rows.shape[0]
+        # host copy of the emulated rows' block counts (longest first): no device read-back
+        self.emu_nb = np.zeros(0, np.int64) if emu_nb is None else np.asarray(emu_nb, np.int64)
         self._scratch = {}
         self._split = None
         self._split_bounds = None
@@ -296,11 +303,11 @@ class HubPlan:
     def emu_parts(self, bounds=(4096, 512)):
         """The emulated rows cut by length into consecutive (row0, row1, block0, block1, short)
         groups: rows of more than bounds[0] blocks, then more than bounds[1], then the rest
-        (rows are stored longest first; short = the last group, whose rows — at most
-        bounds[1] * 256 edges — may run as plain sequential chains, lgcn_chain_rows). The
-        longest walks are the critical path of a layer."""
+        (rows are stored longest first, plan_emulation; short = the last group, whose rows — at
+        most bounds[1] * 256 edges — may run as plain sequential chains, lgcn_chain_rows). The
+        longest walks are the critical path of a layer. Host data only (graph-capture safe)."""
         if self._split is None or self._split_bounds != bounds:
-            nb = self.emu_rows[:, 2].cpu().numpy() if self.n_emu_rows else np.zeros(0, np.int64)
+            nb = self.emu_nb
             cuts = [0] + [int((nb > b).sum()) for b in bounds] + [int(nb.size)]
             firsts = np.concatenate([[0], np.cumsum(nb)])
             self._split = [(r0, r1, int(firsts[r0]), int(firsts[r1]), i == len(bounds))
@@ -346,11 +353,15 @@ class HubPlan:
 
 
 def plan_emulation(rowptr_host, slots, device, row_ids_host=None):
-    """Blocks of LGCN_EMU_BLOCK edges for the emulated rows (slots, largest first)."""
+    """Blocks of LGCN_EMU_BLOCK edges for the emulated rows, longest row first whatever the slot
+    order (the walks of the longest rows are a layer's critical path, and emu_parts cuts the rows
+    by length). Returns (blocks, rows) on the device and the host block counts per row."""
     if slots.size == 0:
-        return None, None
+        return None, None, np.zeros(0, np.int64)
     beg0 = rowptr_host[slots].astype(np.int64)
     deg = rowptr_host[slots + 1].astype(np.int64) - beg0
+    order = np.argsort(-deg, kind="stable")
+    slots, beg0, deg = slots[order], beg0[order], deg[order]
     nb = (deg + LGCN_EMU_BLOCK - 1) // LGCN_EMU_BLOCK
     first = np.concatenate([[0], np.cumsum(nb)[:-1]])
     ix = np.repeat(np.arange(slots.size), nb)
@@ -360,7 +371,7 @@ def plan_emulation(rowptr_host, slots, device, row_ids_host=None):
     blocks = np.stack([ix, beg, end, (k == 0).astype(np.int64)], 1).astype(np.int32)
     out_row = slots if row_ids_host is None else row_ids_host[slots]
     rows = np.stack([out_row, first, nb, np.zeros_like(nb)], 1).astype(np.int32)
-    return torch.from_numpy(blocks).to(device), torch.from_numpy(rows).to(device)
+    return torch.from_numpy(blocks).to(device), torch.from_numpy(rows).to(device), nb
 
 
 def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_group=None,
@@ -387,10 +398,10 @@ def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_grou
         long_ = deg[hub] <= emu_min
         items = np.stack([out_row[long_], rowptr_host[hub[long_]], rowptr_host[hub[long_] + 1],
                           np.full(int(long_.sum()), -1)], 1).astype(np.int32)
-        eb, er = plan_emulation(rowptr_host, hub[~long_], device, row_ids_host)
+        eb, er, enb = plan_emulation(rowptr_host, hub[~long_], device, row_ids_host)
         return HubPlan(threshold, mode, None,
                        torch.from_numpy(items).to(device) if items.shape[0] else None,
-                       emu_blocks=eb, emu_rows=er, emu_min=emu_min)
+                       emu_blocks=eb, emu_rows=er, emu_min=emu_min, emu_nb=enb)
     nch = (deg[hub] + chunk - 1) // chunk
     first = np.concatenate([[0], np.cumsum(nch)[:-1]])
     n_chunks = int(nch.sum())
@@ -703,9 +714,9 @@ emu_trace = None  # a list: spmm_layer records (name, event) pairs of its stream
 
 def emu_slots():
     """LDS re-run slots of the walk per emulated-row part (longest rows first): env
-    LGCN_EMU_SLOTS="a,b,c" (default 15,15,3 — short rows re-run few blocks per chunk, and fewer
+    LGCN_EMU_SLOTS="a,b,c" (default 28,4,2 — short rows resolve few blocks per chunk, and fewer
     slots fit more walk waves per CU)."""
-    v = [int(t) for t in os.environ.get("LGCN_EMU_SLOTS", "15,15,3").split(",") if t.strip()]
+    v = [int(t) for t in os.environ.get("LGCN_EMU_SLOTS", "28,4,2").split(",") if t.strip()]
     return v or [0]
 
 

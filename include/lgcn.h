@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 7
+#define LGCN_ABI_VERSION 8
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -100,8 +100,9 @@ typedef struct {
 
 /* ---- exact hub rows: parallel reproduction of one long sequential chain (lgcn_exact.hip) ---- */
 #define LGCN_EMU_BLOCK 256       /* max edges per emulation block */
-#define LGCN_EMU_CANDS 32        /* candidate chains per (block, column): 16 binades x 2 signs */
+#define LGCN_EMU_CANDS 16        /* translation-table binades per (block, column) */
 #define LGCN_EMU_META_BYTES 16   /* per (block, column) metadata record (opaque) */
+#define LGCN_EMU_MAX_WALK_SLOTS 28 /* lgcn_emu_walk: LDS slots per chunk (CU LDS, vmcnt range) */
 
 /* one block of an emulated row: edges [beg, end) as stored; first = 1 for the row's block 0;
  * row = index of its lgcn_emu_row_t (informational) */
@@ -125,8 +126,9 @@ typedef struct {
  *  - items/n_items: hub chunks (slot >= 0, combined by `rows`) and whole long rows (slot < 0);
  *  - rows/n_rows/n_pre/partials: the chunk combine (lgcn_hub_combine); n_rows = 0 if none;
  *  - emu_*: rows reproduced exactly by block emulation (lgcn_emu_blocks + lgcn_emu_walk);
- *    emu_rel [n_emu_blocks x d x LGCN_EMU_CANDS] 4-byte words and emu_meta [n_emu_blocks x d x
- *    LGCN_EMU_META_BYTES] are caller scratch; emu_stage (optional, NULL = off) [n_emu_blocks x
+ *    emu_rel [n_emu_blocks x d x LGCN_EMU_CANDS] 4-byte words (the per-binade translation
+ *    tables) and emu_meta [n_emu_blocks x d x LGCN_EMU_META_BYTES] are caller scratch, 16-B
+ *    aligned; emu_stage (optional, NULL = off) [n_emu_blocks x
  *    (d + 1) x LGCN_EMU_BLOCK] fp32 scratch: the block pass writes each block's X elements per
  *    column there (and its edge values as column d), so a block the walk must re-run is read
  *    contiguously (LDS-DMA) instead of gathered.
@@ -178,6 +180,9 @@ const char* lgcn_error_string(int code);
                                        2 = off) */
 #define LGCN_TUNE_MIN_GROUPS     4  /* row bundles only when n_rows >= 2 x this many lane groups
                                        (0 = auto = 65536; 1 forces bundles on small graphs) */
+#define LGCN_TUNE_EMU_RESOLVE    5  /* emulation walk: parallel exact-step runs per block it must
+                                       resolve before the rest runs as the sequential chain
+                                       (default 0: always the sequential chain) */
 int lgcn_tune(int knob, int value);
 
 /* device properties the host side needs (CU count); returns 0/hipError */
@@ -299,9 +304,10 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
 
 /* Emulation walk: each emulated row's final value per column (bitwise the sequential chain),
  * epilogue applied, written to Y. Needs lgcn_emu_blocks' rel / meta (and stage, if it wrote
- * one; NULL = re-run blocks gather X) of the same X. slots: LDS slots for predicted re-run
- * blocks per 64-block chunk, 1..63 (0 = LGCN_EMU_SLOTS): 2 KB of LDS per wave each, so a walk
- * over short rows (few re-runs per chunk) runs more waves per CU with fewer slots. */
+ * one; NULL = blocks to resolve gather X) of the same X. slots: LDS slots per 64-block chunk
+ * for the blocks predicted to need an in-block resolve, 1..LGCN_EMU_MAX_WALK_SLOTS (0 = the
+ * default, 12): 4 KB of LDS per wave each (two chunks in flight), so a walk over short rows
+ * runs more waves per CU with fewer slots, and the longest rows (few waves) take many. */
 int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,

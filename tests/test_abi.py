@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 7
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 8
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -147,7 +147,7 @@ def test_tune_knobs(lib):
     """lgcn_tune: every knob answers its previous value (a negative value only queries), an
     unknown knob is refused; knobs never change results (tested on the GPU)."""
     for knob in (engine.TUNE_ROWS_PER_GROUP, engine.TUNE_UNROLL, engine.TUNE_MEAN_PREFETCH,
-                 engine.TUNE_MIN_GROUPS):
+                 engine.TUNE_MIN_GROUPS, engine.TUNE_EMU_RESOLVE):
         old = lib.lgcn_tune(knob, -1)
         assert old >= 0
         assert lib.lgcn_tune(knob, 7) == old

@@ -73,8 +73,11 @@ def test_exact_plan_covers_every_hub_row_once():
     assert list(items[:, 1]) == [rowptr[s] for s in long_slots]
     assert list(items[:, 2]) == [rowptr[s + 1] for s in long_slots]
     blocks, rows = hp.emu_blocks.numpy(), hp.emu_rows.numpy()
-    emu_slots = [s for s in range(deg.size) if deg[s] > 600]
+    # emulated rows are stored longest first whatever the slot order (the walks of the longest
+    # rows are a layer's critical path; emu_parts cuts the rows by length)
+    emu_slots = sorted([s for s in range(deg.size) if deg[s] > 600], key=lambda s: -deg[s])
     assert list(rows[:, 0]) == [row_ids[s] for s in emu_slots]
+    assert list(hp.emu_nb) == [-(-deg[s] // 256) for s in emu_slots]
     for k, s in enumerate(emu_slots):
         _, first, nb, _ = rows[k]
         b = blocks[first:first + nb]

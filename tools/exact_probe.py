@@ -18,8 +18,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from gcn_recommendation_amd import engine  # noqa: E402
 
-NAMES = ["fast", "slow", "identity", "slow:zero/subn", "slow:window", "slow:tie", "slow:bounds",
-         "slow steps"]
+NAMES = ["translated", "resolved", "-", "not predicted", "resolve iterations", "-", "-", "-"]
 
 
 def stats(lib):
@@ -28,8 +27,8 @@ def stats(lib):
     return dict(zip(NAMES, list(buf)))
 
 
-PHASES = ["stage", "predict", "fetch+wait", "scans", "chains", "on-demand fetch", "-", "-",
-          "chunks", "predicted", "re-run", "not predicted"]
+PHASES = ["tables", "predict", "slot wait", "scans", "resolve", "on-demand fetch", "-", "-",
+          "chunks", "predicted", "resolved", "not predicted", "resolve iterations"]
 
 
 def phase_stats(lib):
@@ -51,8 +50,8 @@ def row_stats(lib, hp, d, quiet=False):
     for k in list(range(min(8, len(rows)))) + [min(len(rows), 256) - 1]:
         f, s_, ts, tmax = a[k]
         nb = rows[k, 2]
-        print(f"  row {k}: {nb} blocks x {d} cols: fast {f / d:.0f} slow {s_ / d:.0f} per col "
-              f"({100 * s_ / max(f + s_, 1):.1f}%), slow cycles/slow block "
+        print(f"  row {k}: {nb} blocks x {d} cols: translated {f / d:.0f} resolved {s_ / d:.0f} per "
+              f"col ({100 * s_ / max(f + s_, 1):.1f}%), cycles/resolved block "
               f"{ts / max(s_, 1):.0f}, max wave time {tmax / 2.1e3:.0f} us (at 2.1 GHz)",
               flush=True)
 
