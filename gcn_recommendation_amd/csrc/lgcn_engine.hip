@@ -20,6 +20,7 @@
 #include "lgcn_kernels.h"
 
 #include <string.h>
+#include <new>
 
 namespace lgcn_detail {
 int g_rows_per_group = 0;
@@ -643,43 +644,222 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
     return scale_rows(x, n_rows, d, div, y, ldy, S(stream));
 }
 
-// one layer under a hub plan: emulation block pass -> bundles/chunks/long rows -> combine -> walk
-static int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
-                      int32_t n, const lgcn_hub_plan_t& p, const lgcn_rows_t& x, float xdiv,
-                      const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
-                      const lgcn_epilogue_t& ep, hipStream_t s) {
-    if (p.n_emu_rows > 0) {
-        if (int e = lgcn_emu_blocks(edges, p.emu_blocks, p.n_emu_blocks, x, xdiv, x_nz, d,
-                                    p.emu_rel, p.emu_meta, p.emu_stage, s))
-            return e;
-    }
-    if (int e = spmm_layer(rowptr, edges, row_ids, n, p.threshold, p.items, p.n_items, p.partials,
-                           x, y, ldy, d, ep, xdiv, x_nz, s))
-        return e;
-    if (int e = hub_combine(p.rows, p.n_rows, p.n_pre, p.partials, y, ldy, d, ep, s)) return e;
-    if (p.n_emu_rows > 0) {
-        if (int e = lgcn_emu_walk(edges, p.emu_blocks, p.emu_rows, p.n_emu_rows, p.emu_rel,
-                                  p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, 0, s))
-            return e;
-    }
-    return 0;
+}  // extern "C"
+
+// The concurrent schedule of an exact layer (lgcn_sched_create): auxiliary streams the emulated
+// and chain rows run on beside the layer kernel, and the events that fork them from the caller's
+// stream and join them back (graph-capture safe: a captured fork/join is a graph dependency).
+struct lgcn_sched {
+    hipStream_t aux[3];
+    int n_aux;
+    hipEvent_t fork;
+    hipEvent_t join[3];
+    int32_t slots[2];       // walk LDS slots of part 0 / part 1 (0 = default)
+    int chain;              // 0: chain rows are walked too (tests / A-B)
+    hipEvent_t t0, t1;      // optional: recorded on the caller's stream around the layer kernel
+    hipEvent_t* trace;      // optional [8]: phase events (LGCN_SCHED_TRACE)
+};
+
+namespace {
+struct EmuPart {
+    int32_t r0, r1, b0, b1;
+};
+
+// rows [r0, r1) of the emulated-row list: block pass (blocks [b0, b1)) into the scratch at the
+// part's block offset
+int part_blocks(const lgcn_edge_t* edges, const lgcn_hub_plan_t& p, const EmuPart& q,
+                const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, hipStream_t s) {
+    if (q.b1 <= q.b0) return 0;
+    const int64_t b0 = q.b0;
+    return lgcn_emu_blocks(edges, p.emu_blocks + b0, q.b1 - q.b0, x, xdiv, x_nz, d,
+                           p.emu_rel + b0 * d * LGCN_EMU_CANDS,
+                           static_cast<char*>(p.emu_meta) + b0 * d * LGCN_EMU_META_BYTES,
+                           p.emu_stage ? p.emu_stage + b0 * (d + 1) * LGCN_EMU_BLOCK : nullptr, s);
 }
 
-static int check_plan(const lgcn_hub_plan_t* p) {
+int part_walk(const lgcn_edge_t* edges, const lgcn_hub_plan_t& p, const EmuPart& q,
+              const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y, int64_t ldy,
+              int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
+    if (q.r1 <= q.r0) return 0;
+    return lgcn_emu_walk(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, p.emu_rel,
+                         p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, slots, s);
+}
+
+bool chain_ok(const lgcn_rows_t& x, int32_t d) {
+    return lgcn_chain_supported(d) && x.ld % 4 == 0 && al16(x.p0) && al16(x.p1) && al16(x.p2);
+}
+
+// One layer under a hub plan (every row of Y written once):
+//  - bundles, hub chunks and whole long rows: the layer kernel (spmm_layer) + chunk combine;
+//  - emulated rows, longest first, in three parts (lgcn_hub_plan_t emu_part_*): parts 0 and 1
+//    block pass + walk, part 2 the sequential chain kernel (or walked, when the chain kernel
+//    cannot take d / the alignment, or the schedule turns it off).
+// Without a schedule everything runs in that order on `s`. With one, the emulated parts run on
+// the auxiliary streams beside the layer kernel: part 0 (the longest rows, whose walk is the
+// layer's critical path) on aux[0], part 1 on aux[1], the chain rows on aux[2]; with fewer aux
+// streams the later parts share the last one.
+int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+               int32_t n, const lgcn_hub_plan_t& p, const lgcn_rows_t& x, float xdiv,
+               const uint32_t* x_nz, float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep,
+               const lgcn_sched* sc, hipStream_t s) {
+    const int32_t ne = p.n_emu_rows;
+    const bool chains = ne > p.emu_part_rows[1] && chain_ok(x, d) && (!sc || sc->chain);
+    // walked rows read the block-pass scratch, which must cover their blocks
+    if ((chains ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
+        return LGCN_EINVAL;
+    hipEvent_t* tr = sc ? sc->trace : nullptr;
+    auto mark = [&](int k, hipStream_t st) -> int {
+        return tr && tr[k] ? herr(hipEventRecord(tr[k], st)) : 0;
+    };
+    const EmuPart parts[3] = {{0, p.emu_part_rows[0], 0, p.emu_part_blocks[0]},
+                              {p.emu_part_rows[0], p.emu_part_rows[1], p.emu_part_blocks[0],
+                               p.emu_part_blocks[1]},
+                              {p.emu_part_rows[1], ne, p.emu_part_blocks[1], p.n_emu_blocks}};
+    const int slots[3] = {sc ? sc->slots[0] : 0, sc ? sc->slots[1] : 0, sc ? sc->slots[1] : 0};
+    auto layer_kernel = [&](hipStream_t st) -> int {
+        if (sc && sc->t0) {
+            if (int e = herr(hipEventRecord(sc->t0, st))) return e;
+        }
+        if (int e = spmm_layer(rowptr, edges, row_ids, n, p.threshold, p.items, p.n_items,
+                               p.partials, x, y, ldy, d, ep, xdiv, x_nz, st))
+            return e;
+        if (sc && sc->t1) {
+            if (int e = herr(hipEventRecord(sc->t1, st))) return e;
+        }
+        return hub_combine(p.rows, p.n_rows, p.n_pre, p.partials, y, ldy, d, ep, st);
+    };
+    auto chain_rows = [&](hipStream_t st) -> int {
+        const EmuPart& q = parts[2];
+        if (q.r1 <= q.r0) return 0;
+        return lgcn_chain_rows(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, x, xdiv, y,
+                               ldy, d, &ep, st);
+    };
+    if (!sc || ne == 0) {
+        for (int i = 0; i < 3; ++i)
+            if (i < 2 || !chains)
+                if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, s)) return e;
+        if (int e = layer_kernel(s)) return e;
+        for (int i = 0; i < 3; ++i)
+            if (i < 2 || !chains)
+                if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i], s))
+                    return e;
+        return chains ? chain_rows(s) : 0;
+    }
+    // fork: X and the epilogue operands are ready on `s`
+    const int na = sc->n_aux;
+    auto aux_of = [&](int part) { return sc->aux[part < na ? part : na - 1]; };
+    if (int e = mark(0, s)) return e;
+    if (int e = herr(hipEventRecord(sc->fork, s))) return e;
+    for (int i = 0; i < na; ++i)
+        if (int e = herr(hipStreamWaitEvent(sc->aux[i], sc->fork, 0))) return e;
+    // block passes first (the walk of part 0 starts as soon as its own is done), then the layer
+    // kernel, then the walks and the chains
+    for (int i = 0; i < 3; ++i)
+        if (i < 2 || !chains) {
+            if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, aux_of(i))) return e;
+            if (i < 2)
+                if (int e = mark(1 + i, aux_of(i))) return e;
+        }
+    if (int e = layer_kernel(s)) return e;
+    if (int e = mark(3, s)) return e;
+    if (chains) {
+        if (int e = chain_rows(aux_of(2))) return e;
+        if (int e = mark(4, aux_of(2))) return e;
+    }
+    for (int i = 0; i < 3; ++i)
+        if (i < 2 || !chains) {
+            if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
+                                  aux_of(i)))
+                return e;
+            if (i < 2)
+                if (int e = mark(5 + i, aux_of(i))) return e;
+        }
+    // join: every row of Y written before `s` goes on
+    for (int i = 0; i < na; ++i) {
+        if (int e = herr(hipEventRecord(sc->join[i], sc->aux[i]))) return e;
+        if (int e = herr(hipStreamWaitEvent(s, sc->join[i], 0))) return e;
+    }
+    return mark(7, s);
+}
+
+int check_plan(const lgcn_hub_plan_t* p) {
     if (!p) return LGCN_EINVAL;
     if (p->n_items < 0 || (p->n_items > 0 && !p->items)) return LGCN_EINVAL;
     if (p->n_rows < 0 || p->n_pre < 0 || p->n_pre > p->n_rows) return LGCN_EINVAL;
     if (p->n_rows > 0 && (!p->rows || !p->partials)) return LGCN_EINVAL;
     if (p->n_emu_rows < 0 || p->n_emu_blocks < 0) return LGCN_EINVAL;
-    if (p->n_emu_rows > 0 && (!p->emu_rows || !p->emu_blocks || !p->emu_rel || !p->emu_meta))
+    if (p->n_emu_rows > 0 && (!p->emu_rows || !p->emu_blocks)) return LGCN_EINVAL;
+    const int32_t* pr = p->emu_part_rows;
+    const int32_t* pb = p->emu_part_blocks;
+    if (pr[0] < 0 || pr[0] > pr[1] || pr[1] > p->n_emu_rows || pb[0] < 0 || pb[0] > pb[1] ||
+        pb[1] > p->n_emu_blocks)
         return LGCN_EINVAL;
+    // walked rows need the block-pass scratch
+    if (p->emu_scratch_blocks < 0 || p->emu_scratch_blocks > p->n_emu_blocks) return LGCN_EINVAL;
+    if (p->emu_scratch_blocks > 0 && (!p->emu_rel || !p->emu_meta)) return LGCN_EINVAL;
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** out) {
+    if (!out || n_aux < 1 || n_aux > 3 || !aux_streams) return LGCN_EINVAL;
+    lgcn_sched* sc = new (std::nothrow) lgcn_sched();
+    if (!sc) return LGCN_EINVAL;
+    memset(sc, 0, sizeof(*sc));
+    sc->n_aux = n_aux;
+    sc->chain = 1;
+    for (int i = 0; i < n_aux; ++i) sc->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[i]);
+    int e = herr(hipEventCreateWithFlags(&sc->fork, hipEventDisableTiming));
+    for (int i = 0; i < n_aux && !e; ++i)
+        e = herr(hipEventCreateWithFlags(&sc->join[i], hipEventDisableTiming));
+    if (e) {
+        lgcn_sched_destroy(sc);
+        return e;
+    }
+    *out = sc;
+    return 0;
+}
+
+int lgcn_sched_destroy(lgcn_sched_t* sc) {
+    if (!sc) return 0;
+    if (sc->fork) (void)hipEventDestroy(sc->fork);
+    for (int i = 0; i < 3; ++i)
+        if (sc->join[i]) (void)hipEventDestroy(sc->join[i]);
+    delete sc;
+    return 0;
+}
+
+int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
+    if (!sc) return LGCN_EINVAL;
+    switch (knob) {
+        case LGCN_SCHED_SLOTS0:
+        case LGCN_SCHED_SLOTS1:
+            if (value < 0 || value > LGCN_EMU_MAX_WALK_SLOTS) return LGCN_EINVAL;
+            sc->slots[knob - LGCN_SCHED_SLOTS0] = (int32_t)value;
+            return 0;
+        case LGCN_SCHED_CHAIN:
+            sc->chain = value != 0;
+            return 0;
+        case LGCN_SCHED_TIMING_START:
+            sc->t0 = reinterpret_cast<hipEvent_t>(value);
+            return 0;
+        case LGCN_SCHED_TIMING_END:
+            sc->t1 = reinterpret_cast<hipEvent_t>(value);
+            return 0;
+        case LGCN_SCHED_TRACE:
+            sc->trace = reinterpret_cast<hipEvent_t*>(value);
+            return 0;
+        default:
+            return LGCN_EINVAL;
+    }
 }
 
 int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
                int32_t n_rows, const lgcn_hub_plan_t* plan, lgcn_rows_t x, float x_div,
                const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
-               const lgcn_epilogue_t* epi_host, void* stream) {
+               const lgcn_epilogue_t* epi_host, const lgcn_sched_t* sched, void* stream) {
     if (int e = valid_geom(n_rows, d)) return e;
     if (int e = check_epi(epi_host)) return e;
     if (int e = check_plan(plan)) return e;
@@ -687,14 +867,14 @@ int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     if (!(x_div > 0.f)) return LGCN_EINVAL;
     if (epi_host->mode != LGCN_EPI_ADD && (x_div != 1.f || x_nz)) return LGCN_EINVAL;
     return plan_layer(rowptr, edges, row_ids, n_rows, *plan, x, x_div, x_nz, y, ldy, d,
-                      *epi_host, S(stream));
+                      *epi_host, sched, S(stream));
 }
 
 int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
                            const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                            lgcn_rows_t emb, int32_t d,
                            int32_t K, float* const* layer_bufs_host, float* out,
-                           void* const* ev_host, void* stream) {
+                           void* const* ev_host, const lgcn_sched_t* sched, void* stream) {
     if (int e = valid_geom(n, d)) return e;
     if (K < 0 || K - 1 > LGCN_MAX_LAYERS || !out) return K < 0 || !out ? LGCN_EINVAL : LGCN_ETOOMANY;
     if (K > 1 && !layer_bufs_host) return LGCN_EINVAL;
@@ -721,7 +901,8 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1)], s))) return e;
         }
-        if (int e = plan_layer(rowptr, edges, row_ids, n, *plan, x, 1.f, nullptr, y, d, d, ep, s))
+        if (int e = plan_layer(rowptr, edges, row_ids, n, *plan, x, 1.f, nullptr, y, d, d, ep,
+                               sched, s))
             return e;
         if (ev_host) {
             if (int e = herr(hipEventRecord((hipEvent_t)ev_host[2 * (k - 1) + 1], s))) return e;
@@ -734,7 +915,7 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                             lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
-                            float* grad_e0, void* stream) {
+                            float* grad_e0, const lgcn_sched_t* sched, void* stream) {
     if (int e = valid_geom(n, d)) return e;
     if (K < 0 || !grad_out.p0 || !grad_e0) return LGCN_EINVAL;
     hipStream_t s = S(stream);
@@ -755,7 +936,8 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
     const uint32_t* x_nz = grad_nz;
     for (int k = 1; k <= K; ++k) {
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
-        if (int e = plan_layer(rowptr, edges, row_ids, n, *plan, h, xdiv, x_nz, y, d, d, ep, s))
+        if (int e = plan_layer(rowptr, edges, row_ids, n, *plan, h, xdiv, x_nz, y, d, d, ep, sched,
+                               s))
             return e;
         h = dense_rows(y, n, d);
         xdiv = 1.f;

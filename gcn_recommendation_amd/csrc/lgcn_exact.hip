@@ -299,8 +299,9 @@ __device__ unsigned long long g_emu_phase[16];
 #define PH_MARK(k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
                         ph[k] += now_ - ph_last; ph_last = now_; } while (0)
 #define PH_COUNT(k, v) (ph[k] += (v))
-#define EMU_STAT(k, v) \
-    do { if (threadIdx.x == 0) atomicAdd(&g_emu_stats[k], (unsigned long long)(v)); } while (0)
+// counted per wave in registers, flushed once at the end: an atomic per event would count in
+// vmcnt and make the walker's explicit waits wait for it
+#define EMU_STAT(k, v) (est[k] += (unsigned long long)(v))
 #else
 #define PH_MARK(k) ((void)0)
 #define PH_COUNT(k, v) ((void)0)
@@ -326,11 +327,18 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
-__device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+// inclusive prefix sum of floats over the 64 lanes (DPP, as wave_incl_scan); the order of the
+// additions is the scan's, not sequential: for approximations only
+__device__ __forceinline__ float wave_incl_scan_f(float x) {
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x112, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x118, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xa, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xc, 0xf, false));
+    return x;
 }
+
 
 __device__ __forceinline__ uint32_t lds_byte(const void* p) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)reinterpret_cast<uintptr_t>(p));
@@ -504,6 +512,10 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     auto slot_x = [&](int i) { return s_dyn + i * 2 * B + B; };
     const int lane = threadIdx.x;
     const int c = blockIdx.y;
+#ifdef LGCN_WALK_PRIO
+    // issue priority over the co-resident waves of other kernels on this SIMD (build flag A/B)
+    __builtin_amdgcn_s_setprio(LGCN_WALK_PRIO);
+#endif
     const lgcn_emu_row_t er = rows[blockIdx.x];
     const int64_t fb = er.first_block;
     const int nb_all = er.n_blocks;
@@ -519,6 +531,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long n_fast = 0, n_slow = 0, t_slow = 0, n_iter = 0;
     unsigned long long ph[16] = {0};
+    unsigned long long est[8] = {0};
     unsigned long long ph_last = t_start;
     unsigned long long* iters = &n_iter;
 #else
@@ -575,36 +588,44 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         LGCN_EMU_FORCE(ok);
         return __ballot(act && !ok);
     };
-    // Chunk ch's blocks predicted to need a resolve from the approximate start bits pa (after a
-    // failing block f the value continues as a + r0_f, block f's chain from +0 — the true value
-    // to within its rounding); at most NS are recorded. Returns the approximate end value.
+    // Chunk ch's blocks predicted to need a resolve, from the approximate start bits pa, in ONE
+    // pass: block i's start is taken as pa + the chains from +0 (meta r0) of the blocks before
+    // it — the true contributions to within their rounding — and every lane tests its own block
+    // from its own start with widened bounds. The lowest NS predicted blocks are recorded.
+    // Returns the approximate end value.
     auto predict = [&](int ch, int buf, const int4& m, uint32_t pa,
                        unsigned long long& pred) -> uint32_t {
         const int nb = chunk_nb(ch);
-        pred = 0;
-        int from = 0, np = 0;
-        for (int it = 0; from < nb; ++it) {
-            int incl, dm;
-            const unsigned long long bad = test(pa, from, nb, buf, m, true, incl, dm);
-            if (!bad) return pa + (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-            const int f = (int)__builtin_ctzll(bad);
-            if (np < NS) {
-                pred |= 1ull << f;
-                ++np;
-            }
-            pa += (uint32_t)__builtin_amdgcn_readlane(incl - dm, f);
-            pa = __float_as_uint(__uint_as_float(pa) +
-                                 __int_as_float(__builtin_amdgcn_readlane(m.w, f)));
-            pa = (uint32_t)__builtin_amdgcn_readfirstlane((int)pa);
-            from = f + 1;
-            if (it >= NS + 32) {  // the rest approximated by their chains from +0
-                const float s = wave_sum_f((lane >= from && lane < nb) ? __int_as_float(m.w)
-                                                                       : 0.f);
-                return (uint32_t)__builtin_amdgcn_readfirstlane(
-                    (int)__float_as_uint(__uint_as_float(pa) + s));
-            }
+        const bool act = lane < nb;
+        const float r0 = act ? __int_as_float(m.w) : 0.f;
+        const float incl = wave_incl_scan_f(r0);
+        const uint32_t a = __float_as_uint(__uint_as_float(pa) + (incl - r0));
+        const int E = (int)((a >> 23) & 255u);
+        const int neg = (int)(a >> 31);
+        const int M = (int)((a & 0x7fffffu) | 0x800000u);
+        const int eb = (int)(int16_t)(m.z & 0xffff);
+        const uint32_t vm = (uint32_t)m.z >> 16;
+        const bool ident = eb == kIdentEb;
+        const int w = E - 127 - eb;
+        const bool inw = ((unsigned)(E - 1) < 254u) && ((unsigned)w < (unsigned)kNB) &&
+                         ((vm >> (w & (kNB - 1))) & 1u);
+        const int wc = inw ? w : 0;
+        const int lo = m.x >> wc, hi = -((-m.y) >> wc);
+        const int alo = neg ? -hi : lo, ahi = neg ? -lo : hi;
+        const int mg = ((hi - lo) >> 3) + 256;
+        const bool ok = ident || (inw && M + alo >= kLB + mg && M + ahi <= kHB - mg);
+        unsigned long long bad = __ballot(act && !ok);
+        // keep the NS lowest
+        unsigned long long keep = 0;
+        for (int i = 0; i < NS && bad; ++i) {
+            const unsigned long long lowbit = bad & (~bad + 1ull);
+            keep |= lowbit;
+            bad ^= lowbit;
         }
-        return pa;
+        pred = keep;
+        const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+        return (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__float_as_uint(__uint_as_float(pa) + tot));
     };
     auto fetch = [&](int64_t bi, int slot) {  // block bi's staged values -> LDS slot (2 DMAs)
         dma16(stage + (bi * (d + 1) + d) * B + 4 * lane, lds_byte(slot_v(slot)));
@@ -734,9 +755,11 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA lands after the wave is gone
 #ifdef LGCN_EMU_STATS
     ph[12] = n_iter;
+    est[4] += n_iter;
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
         for (int k = 0; k < 16; ++k) g_emu_phase[k] += ph[k];
-    if (lane == 0) atomicAdd(&g_emu_stats[4], n_iter);
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_emu_stats[k], est[k]);
     if (lane == 0 && blockIdx.x < 256) {
         atomicAdd(&g_emu_row_stats[blockIdx.x][0], n_fast);
         atomicAdd(&g_emu_row_stats[blockIdx.x][1], n_slow);
@@ -854,7 +877,7 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int MODE, int XD, int W>
+template <int MODE, int XD, int W, bool SEG1>
 __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict__ edges,
                                                    const lgcn_emu_block_t* __restrict__ blocks,
                                                    const lgcn_emu_row_t* __restrict__ rows,
@@ -865,36 +888,41 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     constexpr int NX = C::NX, NR = C::NR, AHEAD = C::AHEAD;
     static_assert(AHEAD * (C::NI + 2) <= 63, "vmcnt holds at most 63 outstanding loads");
     __shared__ __attribute__((aligned(16))) float s_x[NX][C::XWIN];
-    __shared__ __attribute__((aligned(16))) int2 s_rec[NR][64];
+    __shared__ __attribute__((aligned(16))) int32_t s_col[NR][64];
+    __shared__ __attribute__((aligned(16))) float s_val[NR][64];
     const int lane = threadIdx.x;
     const int c0 = blockIdx.y * W;
     const lgcn_emu_row_t er = rows[blockIdx.x];
     const int32_t beg = blocks[er.first_block].beg;
     const int32_t end = blocks[er.first_block + er.n_blocks - 1].end;
     const int32_t nwin = (end - beg + 63) >> 6;
-    // records of window w -> s_rec[w % NR]: 128 dwords in two dword LDS-DMA loads. Dwords past
-    // the row repeat its last record (col and val kept apart by parity), so windows past the
-    // end load valid records and gather valid rows: every iteration issues the same number of
-    // loads, which keeps the vmcnt arithmetic below exact. They are never folded.
+    // records of window w: lane l's column -> s_col[w % NR][l], its value -> s_val[w % NR][l]
+    // (two dword LDS-DMA loads). Windows past the row repeat its last record, so they load
+    // valid records and gather valid rows: every iteration issues the same number of loads,
+    // which keeps the vmcnt arithmetic below exact. They are never folded.
     const int32_t* ew = reinterpret_cast<const int32_t*>(edges);
-    const int64_t dl = 2 * (int64_t)end - 1, dlast = 2 * (int64_t)end - 2 + (lane & 1);
     auto rec_dma = [&](int32_t w) {
-        const int64_t d0 = 2 * ((int64_t)beg + 64 * w) + lane;
-        const uint32_t dst = lds_byte(&s_rec[w % NR][0]);
-        dma4(ew + (d0 <= dl ? d0 : dlast), dst);
-        dma4(ew + (d0 + 64 <= dl ? d0 + 64 : dlast), dst + 256);
+        const int64_t j = min((int64_t)beg + 64 * w + lane, (int64_t)end - 1);
+        dma4(ew + 2 * j, lds_byte(&s_col[w % NR][0]));
+        dma4(ew + 2 * j + 1, lds_byte(&s_val[w % NR][0]));
     };
     // gathered X of window w -> s_x[w % NX]: instruction k moves rows k*RPI .. k*RPI + RPI - 1
     // (lane -> row sub = lane / LPR, 16-B piece q = lane % LPR); the columns come from LDS
     const int sub = lane / C::LPR, q = lane % C::LPR;
+    const char* xb = reinterpret_cast<const char*>(x.p0) + (c0 + 4 * q) * 4;
+    const uint32_t row_b = (uint32_t)(x.ld * 4);  // d <= 2048: a row is at most 8 KB
     auto x_dma = [&](int32_t w) {
         int32_t cols[C::NI];
 #pragma unroll
-        for (int k = 0; k < C::NI; ++k) cols[k] = s_rec[w % NR][k * C::RPI + sub].x;
+        for (int k = 0; k < C::NI; ++k) cols[k] = s_col[w % NR][k * C::RPI + sub];
         const uint32_t dst = lds_byte(s_x[w % NX]);
 #pragma unroll
-        for (int k = 0; k < C::NI; ++k)
-            dma16(seg_row_sel(x, cols[k]) + c0 + 4 * q, dst + k * 1024);
+        for (int k = 0; k < C::NI; ++k) {
+            if constexpr (SEG1)  // one buffer: a row is base + col * ld
+                dma16(xb + (uint64_t)(uint32_t)cols[k] * row_b, dst + k * 1024);
+            else
+                dma16(seg_row_sel(x, cols[k]) + c0 + 4 * q, dst + k * 1024);
+        }
     };
     // Pipeline (A = AHEAD): iteration v issues x(v + A) then rec(v + 2A); the prologue runs
     // v = -A .. -1 after rec(0 .. A-1) have landed. At iteration w, x(w) and rec(w + A) (both
@@ -918,42 +946,46 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
         rec_dma(w + 2 * AHEAD);
         const int n = min(64, end - beg - 64 * w);
         const float* xs = &s_x[w % NX][cc];  // step j's element of column cc: xs[j * W]
-        // lane l holds step l's edge value; a step reads it by v_readlane (a scalar operand)
-        const float vw = __int_as_float(s_rec[w % NR][lane].y);
-        // groups of 8 steps: group g + 1's LDS reads are issued before group g is folded (the
-        // sched_barriers keep the compiler from sinking them next to their use)
-        float xg[2][8];
-        auto load8 = [&](float (&r)[8], int g) {
+        const float4* vs = reinterpret_cast<const float4*>(s_val[w % NR]);  // broadcast reads
+        // groups of 8 steps, two groups' LDS reads (2 x 16-B edge values + 8 X elements, the
+        // latter paired by ds_read2) issued ahead of the group being folded; the sched_barriers
+        // keep the compiler from sinking them next to their use
+        float xg[3][8];
+        float4 vg[3][2];
+        auto load8 = [&](int slot, int g) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t) r[t] = xs[(8 * g + t) * W];
+            for (int t = 0; t < 8; ++t) xg[slot][t] = xs[(8 * g + t) * W];
+            vg[slot][0] = vs[2 * g];
+            vg[slot][1] = vs[2 * g + 1];
         };
-        auto fold8 = [&](const float (&r)[8], int g, bool full) {
+        auto fold8 = [&](int slot, int g, bool full) {
+            const float vv[8] = {vg[slot][0].x, vg[slot][0].y, vg[slot][0].z, vg[slot][0].w,
+                                 vg[slot][1].x, vg[slot][1].y, vg[slot][1].z, vg[slot][1].w};
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                float xe = r[t];
+                float xe = xg[slot][t];
                 if constexpr ((XD & 3) == 1) xe = xe / xdiv;
                 else if constexpr ((XD & 3) == 2) xe = xe * xdiv;
-                const int j = 8 * g + t;
-                const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vw), j));
-                const float f = __builtin_fmaf(v, xe, acc);
-                acc = (full || j < n) ? f : acc;
+                const float f = __builtin_fmaf(vv[t], xe, acc);
+                acc = (full || 8 * g + t < n) ? f : acc;
             }
         };
-        load8(xg[0], 0);
+        load8(0, 0);
+        load8(1, 1);
         if (n == 64) {
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                if (g + 1 < 8) load8(xg[(g + 1) & 1], g + 1);
+                if (g + 2 < 8) load8((g + 2) % 3, g + 2);
                 __builtin_amdgcn_sched_barrier(0);
-                fold8(xg[g & 1], g, true);
+                fold8(g % 3, g, true);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {  // the row's last window: steps past n leave acc alone
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                if (g + 1 < 8) load8(xg[(g + 1) & 1], g + 1);
+                if (g + 2 < 8) load8((g + 2) % 3, g + 2);
                 __builtin_amdgcn_sched_barrier(0);
-                fold8(xg[g & 1], g, false);
+                fold8(g % 3, g, false);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -985,12 +1017,18 @@ int launch_chain(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     // or more waves per row, each with twice the windows in flight of a 64-column wave
     const int w = d % 32 == 0 ? 32 : 16;  // 16, 32 or a multiple of 64 (checked by the caller)
     const dim3 grid((uint32_t)n_rows, (uint32_t)((d + w - 1) / w));
-    if (w == 32)
-        hipLaunchKernelGGL((k_chain_rows<MODE, XD, 32>), grid, dim3(64), 0, s, edges, blocks, rows,
-                           x, xdiv, d, y, ldy, ep);
-    else
-        hipLaunchKernelGGL((k_chain_rows<MODE, XD, 16>), grid, dim3(64), 0, s, edges, blocks, rows,
-                           x, xdiv, d, y, ldy, ep);
+    const bool seg1 = x.p0 == x.p1 && x.p1 == x.p2;
+#define LGCN_CH(W_, S_) \
+    hipLaunchKernelGGL((k_chain_rows<MODE, XD, W_, S_>), grid, dim3(64), 0, s, edges, blocks, \
+                       rows, x, xdiv, d, y, ldy, ep)
+    if (w == 32) {
+        if (seg1) LGCN_CH(32, true);
+        else LGCN_CH(32, false);
+    } else {
+        if (seg1) LGCN_CH(16, true);
+        else LGCN_CH(16, false);
+    }
+#undef LGCN_CH
     return herr_x(hipGetLastError());
 }
 

@@ -25,6 +25,11 @@ COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
 TUNE_EMU_RESOLVE = 5
+SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
+    1, 2, 3, 4, 5, 6
+# phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
+TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
+                "part0_walk", "part1_walk", "joined")
 ABI_VERSION = 8
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
@@ -38,9 +43,11 @@ LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 # power-law hubs, kept as the unoptimised reference mode).
 DEFAULT_HUB_THRESHOLD = 128
 HUB_MODES = ("exact", "chunk")
-# Whole-row chains above this degree are emulated (LGCN_EMU_MIN_DEGREE): a chain is one lane
-# group's dependent gathers (~0.27 us per 8 edges), so 4096 edges is ~0.14 ms.
-DEFAULT_EMU_MIN_DEGREE = 4096
+# Rows above the bundle threshold and up to this degree run inside the layer kernel as one lane
+# group's chain each (LGCN_EMU_MIN_DEGREE); 0 (default) = none: every row above the threshold
+# goes to the emulated-row list, where the shorter ones run as sequential chains of their own
+# (lgcn_chain_rows, beside the layer kernel) and the longest are block-emulated (emu_parts).
+DEFAULT_EMU_MIN_DEGREE = 0
 
 
 def hub_mode_from_env():
@@ -59,6 +66,17 @@ def emu_stage_enabled():
 def emu_min_degree_from_env():
     v = os.environ.get("LGCN_EMU_MIN_DEGREE", "")
     return int(v) if v else DEFAULT_EMU_MIN_DEGREE
+
+
+def chain_max_degree(nnz):
+    """Rows of the emulated-row list up to this degree run as sequential chains (lgcn_chain_rows,
+    ~16 ns per edge), longer ones are block-emulated (block pass + walk): env LGCN_CHAIN_MAX, else
+    by graph size — a chain must stay short against the whole layer (C3: 56M nonzeros, ~3 ms per
+    layer -> 55k edges; C2: 1.6M, ~0.07 ms -> the 2048 floor)."""
+    v = os.environ.get("LGCN_CHAIN_MAX", "")
+    if v:
+        return int(v)
+    return int(min(max(nnz // 1024, 2048), 65536))
 # Edges per hub chunk: LGCN_HUB_CHUNK, else by graph size (hub_chunk_for). A chunk is one lane
 # group's sequential chain, so it must stay short against the whole layer: on the C2 graph
 # (1.6M nonzeros, 0.07-0.1 ms per layer) 128-edge chunks run the forward 0.318 -> 0.224 ms,
@@ -94,7 +112,9 @@ class PlanT(ctypes.Structure):
                 ("emu_stage", ctypes.c_void_p),
                 ("threshold", ctypes.c_int32), ("n_items", ctypes.c_int32),
                 ("n_rows", ctypes.c_int32), ("n_pre", ctypes.c_int32),
-                ("n_emu_blocks", ctypes.c_int32), ("n_emu_rows", ctypes.c_int32)]
+                ("n_emu_blocks", ctypes.c_int32), ("n_emu_rows", ctypes.c_int32),
+                ("emu_part_rows", ctypes.c_int32 * 2), ("emu_part_blocks", ctypes.c_int32 * 2),
+                ("emu_scratch_blocks", ctypes.c_int32)]
 
 
 class LgcnError(RuntimeError):
@@ -143,12 +163,15 @@ ABI = [
     ("lgcn_chain_supported", ctypes.c_int, [_I32]),
     ("lgcn_chain_rows", ctypes.c_int, [_P, _P, _P, _I32, RowsT, ctypes.c_float, _P, _I64, _I32,
                                        ctypes.POINTER(EpilogueT), _P]),
+    ("lgcn_sched_create", ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("lgcn_sched_destroy", ctypes.c_int, [_P]),
+    ("lgcn_sched_set", ctypes.c_int, [_P, _I32, _I64]),
     ("lgcn_layer", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, ctypes.c_float, _P,
-                                  _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
+                                  _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P, _P]),
     ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _I32,
-                                              _I32, _P, _P, _P, _P]),
+                                              _I32, _P, _P, _P, _P, _P]),
     ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _P,
-                                               _I32, _I32, _P, _P, _P]),
+                                               _I32, _I32, _P, _P, _P, _P]),
 ]
 
 
@@ -319,24 +342,56 @@ class HubPlan:
     def n_long(self):
         return self.n_items if self.mode == "exact" else 0
 
-    def scratch(self, d, device):
-        """(partials, emu_rel, emu_meta, emu_stage) for width d, allocated once per width and
-        reused (the layers of one operator run in stream order)."""
-        if d not in self._scratch:
+    def walk_parts(self, nnz):
+        """(part_rows, part_blocks): the emulated rows cut into part 0 (rows of more than
+        LGCN_EMU_PART0 = 8192 blocks, the longest walks: the layer's critical path), part 1 (more
+        than chain_max_degree blocks) and the chain rows (lgcn_hub_plan_t emu_part_*)."""
+        b1 = -(-chain_max_degree(nnz) // LGCN_EMU_BLOCK)
+        b0 = max(int(os.environ.get("LGCN_EMU_PART0", "8192")), b1)
+        nb = self.emu_nb
+        cum = np.concatenate([[0], np.cumsum(nb)])
+        r0, r1 = int((nb > b0).sum()), int((nb > b1).sum())
+        return [r0, r1], [int(cum[r0]), int(cum[r1])]
+
+    def scratch(self, d, device, n_blocks=None):
+        """(partials, emu_rel, emu_meta, emu_stage) for width d, covering the first n_blocks
+        emulated blocks (the walked ones; default all), allocated once per width and grown on
+        demand (the layers of one operator run in stream order). release_scratch() drops it."""
+        n_blocks = self.n_emu_blocks if n_blocks is None else n_blocks
+        have = self._scratch.get(d)
+        if have is None or have[4] < n_blocks:
             f32 = dict(dtype=torch.float32, device=device)
-            part = torch.empty(self.n_slots * d, **f32) if self.n_slots else None
+            part = have[0] if have is not None else (
+                torch.empty(self.n_slots * d, **f32) if self.n_slots else None)
             rel = meta = stage = None
-            if self.n_emu_blocks:
-                rel = torch.empty(self.n_emu_blocks * d * LGCN_EMU_CANDS, **f32)
-                meta = torch.empty(self.n_emu_blocks * d * LGCN_EMU_META_BYTES, dtype=torch.uint8,
+            if n_blocks:
+                rel = torch.empty(n_blocks * d * LGCN_EMU_CANDS, **f32)
+                meta = torch.empty(n_blocks * d * LGCN_EMU_META_BYTES, dtype=torch.uint8,
                                    device=device)
                 if emu_stage_enabled():
-                    stage = torch.empty(self.n_emu_blocks * (d + 1) * LGCN_EMU_BLOCK, **f32)
-            self._scratch[d] = (part, rel, meta, stage)
-        return self._scratch[d]
+                    stage = torch.empty(n_blocks * (d + 1) * LGCN_EMU_BLOCK, **f32)
+            self._scratch[d] = (part, rel, meta, stage, n_blocks)
+        return self._scratch[d][:4]
 
-    def struct(self, d, device):
-        part, rel, meta, stage = self.scratch(d, device)
+    def release_scratch(self, d=None):
+        """Drop the cached scratch of width d (all widths: None); torch.cuda.empty_cache() can
+        then return it."""
+        if d is None:
+            self._scratch.clear()
+        else:
+            self._scratch.pop(d, None)
+
+    def struct(self, d, device, nnz=None, walk_all=False):
+        """lgcn_hub_plan_t for width d. nnz: the operator's nonzeros (sets the chain/walk cut;
+        None = every emulated row walked). walk_all: the chain rows are walked too (no chain
+        kernel for this d / alignment, or LGCN_CHAIN=0), so the scratch covers every block."""
+        if nnz is None or walk_all:
+            rows = [self.n_emu_rows, self.n_emu_rows] if nnz is None else None
+            blocks = [self.n_emu_blocks, self.n_emu_blocks] if nnz is None else None
+        if nnz is not None:
+            rows, blocks = self.walk_parts(nnz)
+        need = self.n_emu_blocks if (walk_all or nnz is None) else blocks[1]
+        part, rel, meta, stage = self.scratch(d, device, need)
         p = PlanT()
         p.items, p.n_items = (self.items.data_ptr() if self.n_items else None), self.n_items
         p.rows, p.n_rows, p.n_pre = (self.rows.data_ptr() if self.n_entries else None), \
@@ -349,6 +404,9 @@ class HubPlan:
         p.emu_meta = meta.data_ptr() if meta is not None else None
         p.emu_stage = stage.data_ptr() if stage is not None else None
         p.threshold = min(self.threshold, INT32_MAX)
+        p.emu_part_rows[0], p.emu_part_rows[1] = rows
+        p.emu_part_blocks[0], p.emu_part_blocks[1] = blocks
+        p.emu_scratch_blocks = need
         return p
 
 
@@ -684,23 +742,71 @@ def _check_emb(segments, d, device):
             raise LgcnError("embedding blocks must be contiguous [rows x d]")
 
 
-_side_streams = {}
+_scheds = {}
 
 
 def _side_stream(device, i=0):
-    """Per-device side streams the emulated hub rows run on, beside the layer kernel. Stream 0
-    carries the longest rows (the layer's critical path): it is created at high priority
-    (LGCN_EMU_PRIORITY=0: normal) so its waves are dispatched ahead of the layer kernel's."""
+    """Per-device side streams the emulated and chain rows run on beside the layer kernel
+    (lgcn_sched). Stream 0 carries the longest rows (the layer's critical path): it is created
+    at high priority (LGCN_EMU_PRIORITY=0: normal) so its waves are dispatched first."""
     key = (str(device), i)
-    if key not in _side_streams:
+    sc = _scheds.setdefault(("streams", str(device)), {})
+    if i not in sc:
         hi = i < int(os.environ.get("LGCN_EMU_PRIORITY", "1"))  # streams 0..n-1 high priority
-        _side_streams[key] = torch.cuda.Stream(device, priority=-1 if hi else 0)
-    return _side_streams[key]
+        sc[i] = torch.cuda.Stream(device, priority=-1 if hi else 0)
+    return sc[i]
+
+
+def n_aux_streams():
+    """Auxiliary streams of the exact layer (LGCN_AUX_STREAMS, 1..3, default 3): with the
+    caller's stream 4 hardware queues (GPU_MAX_HW_QUEUES=4); at N > 1 RCCL's stream competes
+    for them, and the N > 1 path asks for 2."""
+    return max(1, min(3, int(os.environ.get("LGCN_AUX_STREAMS", "3"))))
+
+
+class Sched:
+    """lgcn_sched_t over this device's side streams (created once per device and stream count;
+    the C library owns the fork/join events)."""
+
+    def __init__(self, device, n_aux):
+        lib = load_library()
+        self.lib, self.device, self.n_aux = lib, device, n_aux
+        self.streams = [_side_stream(device, i) for i in range(n_aux)]
+        arr = (ctypes.c_void_p * n_aux)(*[st.cuda_stream for st in self.streams])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _check(lib.lgcn_sched_create(arr, n_aux, ctypes.byref(h)), "lgcn_sched_create")
+        self.handle = h
+        slots = emu_slots()
+        self.set(SCHED_SLOTS0, slots[0])
+        self.set(SCHED_SLOTS1, slots[min(1, len(slots) - 1)])
+        self.set(SCHED_CHAIN, 1 if chain_enabled() else 0)
+
+    def set(self, knob, value):
+        _check(self.lib.lgcn_sched_set(self.handle, knob, int(value)), "lgcn_sched_set")
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.lib.lgcn_sched_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def sched_for(device):
+    """The device's Sched (None with LGCN_EMU_OVERLAP=0: every part in order on the caller's
+    stream)."""
+    if not emu_overlap_enabled():
+        return None
+    key = (str(device), n_aux_streams(), emu_slots_key(), chain_enabled())
+    if key not in _scheds:
+        _scheds[key] = Sched(device, key[1])
+    return _scheds[key]
 
 
 def chain_enabled():
-    """Emulated rows of the short part (<= 512 blocks) run as plain sequential chains
-    (lgcn_chain_rows) instead of block pass + walk; LGCN_CHAIN=0 emulates them too."""
+    """Rows of the emulated-row list below the chain cut run as plain sequential chains
+    (lgcn_chain_rows) instead of block pass + walk; LGCN_CHAIN=0 walks them too."""
     return os.environ.get("LGCN_CHAIN", "1") != "0"
 
 
@@ -709,109 +815,75 @@ def _aligned16(segments):
                for t in segments)
 
 
-emu_trace = None  # a list: spmm_layer records (name, event) pairs of its streams' phases into it
-
-
 def emu_slots():
-    """LDS re-run slots of the walk per emulated-row part (longest rows first): env
-    LGCN_EMU_SLOTS="a,b,c" (default 28,4,2 — short rows resolve few blocks per chunk, and fewer
-    slots fit more walk waves per CU)."""
-    v = [int(t) for t in os.environ.get("LGCN_EMU_SLOTS", "28,4,2").split(",") if t.strip()]
+    """LDS slots of the walk (part 0, part 1): env LGCN_EMU_SLOTS="a,b" (default 28,12 — the
+    longest rows run few waves and take many slots; part 1's rows are more waves, and fewer
+    slots fit more of them per CU)."""
+    v = [int(t) for t in os.environ.get("LGCN_EMU_SLOTS", "28,12").split(",") if t.strip()]
     return v or [0]
+
+
+def emu_slots_key():
+    return os.environ.get("LGCN_EMU_SLOTS", "")
 
 
 def emu_overlap_enabled():
     """LGCN_EMU_OVERLAP=0 runs the emulated rows on the caller's stream, after the layer kernel
-    (lgcn_layer's order) instead of beside it on a side stream."""
+    (no lgcn_sched) instead of beside it on side streams."""
     return os.environ.get("LGCN_EMU_OVERLAP", "1") != "0"
+
+
+emu_trace = None  # a list: spmm_layer appends (phase, torch.cuda.Event) of the layer (SCHED_TRACE)
 
 
 def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0,
                x_nz=None, kernel_events=None):
-    """One layer Y = epilogue(Â·(X / x_div)) under the operator's hub plan: the emulation block
-    pass, the layer kernel (bundles, long rows, chunks), the chunk combine and the emulation
-    walk. The emulated rows touch no row the layer kernel writes, so by default they run on a
-    side stream concurrently with it (forked from and joined back into the caller's stream:
-    graph-capture safe); LGCN_EMU_OVERLAP=0 serialises them (lgcn_layer).
+    """One layer Y = epilogue(Â·(X / x_div)) under the operator's hub plan — lgcn_layer: the layer
+    kernel (bundles, chunks, whole long rows) + chunk combine, the block pass + walk of the
+    emulated parts and the chain rows, concurrently on the device's side streams (lgcn_sched,
+    forked from and joined back into the caller's stream: graph-capture safe).
     x_nz: optional row bitmask of X (rows_nonzero; ADD epilogue only). kernel_events: optional
     (start, end) torch.cuda.Event pair recorded on the caller's stream around the layer kernel
-    launch (lgcn_layer: bundles, long rows, chunks) — bench.py's live timing of that kernel."""
+    (bench.py's live timing of that kernel)."""
     lib = load_library()
     hp = hubs or graph.hubs(hub_threshold)
     stream = stream or _stream(graph.device)
-    plan = hp.struct(d, graph.device)
-    x = rows_desc(x_segments, d)
-    args = (_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), graph.n_rows)
-    if not (hp.n_emu_rows and emu_overlap_enabled()):
-        if kernel_events is not None:
-            kernel_events[0].record()
-        _check(lib.lgcn_layer(*args, ctypes.byref(plan), x, x_div, _ptr(x_nz), _ptr(y),
-                              y.stride(0), d, ctypes.byref(epi), stream), "lgcn_layer")
-        if kernel_events is not None:
-            kernel_events[1].record()
-        return y
     main = torch.cuda.current_stream(graph.device)
     if main.cuda_stream != (stream.value or 0):
         raise LgcnError("spmm_layer: stream must be the device's current stream")
-    # the longest rows' walks are the critical path: their block pass runs first, alone, and
-    # their walk starts as soon as it is done, on a side stream of their own; shorter emulated
-    # rows follow on further side streams (rows are stored longest first)
-    parts = hp.emu_parts(tuple(int(b) for b in os.environ.get(
-        "LGCN_EMU_PART_BOUNDS", "8192,1024").split(",")))  # probe: 4096,512 -> 8192,1024: -1.1 ms
-    chain = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
-    sides = [_side_stream(graph.device, i) for i in range(len(parts))]
-    tr = emu_trace
-    if tr is not None:  # diagnostics (tools/exact_layer_probe.py): per-stream phase events
-        tr.clear()
-        tr.append(("start", main.record_event(torch.cuda.Event(enable_timing=True))))
-    for sd in sides:
-        sd.wait_stream(main)        # X (and the epilogue operands) are ready
-    rb, bb = hp.emu_rows.element_size() * 4, hp.emu_blocks.element_size() * 4
-    for sd, (r0, r1, b0, b1, short) in zip(sides, parts):
-        if r1 <= r0 or (short and chain):
-            continue
-        ss = ctypes.c_void_p(sd.cuda_stream)
-        # records are indexed by block: a sub-range of blocks writes at its own offset
-        _check(lib.lgcn_emu_blocks(
-            _ptr(graph.edges), plan.emu_blocks + b0 * bb, b1 - b0, x, x_div, _ptr(x_nz), d,
-            plan.emu_rel + b0 * d * LGCN_EMU_CANDS * 4, plan.emu_meta + b0 * d * LGCN_EMU_META_BYTES,
-            plan.emu_stage + b0 * (d + 1) * LGCN_EMU_BLOCK * 4 if plan.emu_stage else None, ss),
-            "lgcn_emu_blocks")
-        if tr is not None:
-            tr.append((f"part{len(tr) - 1}_blocks", sd.record_event(
-                torch.cuda.Event(enable_timing=True))))
-    rest = PlanT.from_buffer_copy(plan)
-    rest.n_emu_rows = rest.n_emu_blocks = 0
-    if kernel_events is not None:
+    chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
+    plan = hp.struct(d, graph.device, nnz=graph.nnz, walk_all=not chains)
+    x = rows_desc(x_segments, d)
+    sc = sched_for(graph.device) if hp.n_emu_rows else None
+    args = (_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), graph.n_rows)
+    trace = None
+    if sc is not None and (kernel_events is not None or emu_trace is not None):
+        if kernel_events is not None:
+            for ev in kernel_events:  # materialise the hipEvent_t handles
+                ev.record()
+            sc.set(SCHED_TIMING_START, kernel_events[0].cuda_event)
+            sc.set(SCHED_TIMING_END, kernel_events[1].cuda_event)
+        if emu_trace is not None:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in TRACE_PHASES]
+            for ev in evs:
+                ev.record()
+            trace = (ctypes.c_void_p * len(evs))(*[ev.cuda_event for ev in evs])
+            sc.set(SCHED_TRACE, ctypes.addressof(trace))
+    elif kernel_events is not None:
         kernel_events[0].record()
-    _check(lib.lgcn_layer(*args, ctypes.byref(rest), x, x_div, _ptr(x_nz), _ptr(y), y.stride(0),
-                          d, ctypes.byref(epi), stream), "lgcn_layer")
-    if kernel_events is not None:
-        kernel_events[1].record()
-    if tr is not None:
-        tr.append(("layer_kernel", main.record_event(torch.cuda.Event(enable_timing=True))))
-    slots = emu_slots()
-    for i, (sd, (r0, r1, b0, b1, short)) in enumerate(zip(sides, parts)):
-        if r1 <= r0:
-            continue
-        if short and chain:
-            _check(lib.lgcn_chain_rows(_ptr(graph.edges), plan.emu_blocks, plan.emu_rows + r0 * rb,
-                                       r1 - r0, x, x_div, _ptr(y), y.stride(0), d,
-                                       ctypes.byref(epi), ctypes.c_void_p(sd.cuda_stream)),
-                   "lgcn_chain_rows")
-            if tr is not None:
-                tr.append((f"part{i}_chain", sd.record_event(
-                    torch.cuda.Event(enable_timing=True))))
-            continue
-        _check(lib.lgcn_emu_walk(_ptr(graph.edges), plan.emu_blocks, plan.emu_rows + r0 * rb,
-                                 r1 - r0, plan.emu_rel, plan.emu_meta, plan.emu_stage, x, x_div,
-                                 _ptr(x_nz), _ptr(y), y.stride(0), d, ctypes.byref(epi),
-                                 slots[min(i, len(slots) - 1)],
-                                 ctypes.c_void_p(sd.cuda_stream)), "lgcn_emu_walk")
-        if tr is not None:
-            tr.append((f"part{i}_walk", sd.record_event(torch.cuda.Event(enable_timing=True))))
-    for sd in sides:
-        main.wait_stream(sd)        # every row of Y written
+    try:
+        _check(lib.lgcn_layer(*args, ctypes.byref(plan), x, x_div, _ptr(x_nz), _ptr(y),
+                              y.stride(0), d, ctypes.byref(epi),
+                              sc.handle if sc is not None else None, stream), "lgcn_layer")
+    finally:
+        if sc is not None:
+            sc.set(SCHED_TIMING_START, 0)
+            sc.set(SCHED_TIMING_END, 0)
+            sc.set(SCHED_TRACE, 0)
+    if sc is None and kernel_events is not None:
+        kernel_events[1].record()  # (no schedule: the whole layer)
+    if trace is not None:
+        emu_trace[:] = list(zip(TRACE_PHASES, evs))
     return y
 
 

@@ -125,7 +125,8 @@ typedef struct {
 /* Everything a layer needs beyond the CSR to treat rows above the bundle threshold:
  *  - items/n_items: hub chunks (slot >= 0, combined by `rows`) and whole long rows (slot < 0);
  *  - rows/n_rows/n_pre/partials: the chunk combine (lgcn_hub_combine); n_rows = 0 if none;
- *  - emu_*: rows reproduced exactly by block emulation (lgcn_emu_blocks + lgcn_emu_walk);
+ *  - emu_*: rows summed exactly outside the layer kernel: block emulation (lgcn_emu_blocks +
+ *    lgcn_emu_walk) or the sequential chain kernel (lgcn_chain_rows), see emu_part_*;
  *    emu_rel [n_emu_blocks x d x LGCN_EMU_CANDS] 4-byte words (the per-binade translation
  *    tables) and emu_meta [n_emu_blocks x d x LGCN_EMU_META_BYTES] are caller scratch, 16-B
  *    aligned; emu_stage (optional, NULL = off) [n_emu_blocks x
@@ -149,6 +150,17 @@ typedef struct {
     int32_t n_pre;
     int32_t n_emu_blocks;
     int32_t n_emu_rows;
+    /* The emulated rows (stored longest first) in three parts: rows [0, emu_part_rows[0]) and
+     * [emu_part_rows[0], emu_part_rows[1]) are block-passed and walked (their blocks: [0,
+     * emu_part_blocks[0]) and [emu_part_blocks[0], emu_part_blocks[1])); the rows after
+     * emu_part_rows[1] run as sequential chains (lgcn_chain_rows) when lgcn_chain_supported(d)
+     * and X is 16-B aligned, and are walked otherwise. The scratch (emu_rel / emu_meta /
+     * emu_stage) must cover the walked blocks: [0, emu_part_blocks[1]) when chains run, all
+     * n_emu_blocks otherwise; emu_scratch_blocks = the blocks it covers (a layer that would walk
+     * past it returns LGCN_EINVAL). {0, 0} = every emulated row is a chain row. */
+    int32_t emu_part_rows[2];
+    int32_t emu_part_blocks[2];
+    int32_t emu_scratch_blocks;
 } lgcn_hub_plan_t;
 
 /* Epilogue operands. MEAN: prev0 is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
@@ -326,34 +338,56 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                     float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
                     void* stream);
 
-/* One whole layer under a hub plan: emulation block pass, lgcn_spmm_layer (bundles, chunks and
- * long rows), chunk combine, emulation walk — every row of Y written once. */
+/* Concurrent schedule of the exact layers (lgcn_layer, lgcn_propagate_forward/backward): the
+ * emulated and chain rows run on 1..3 auxiliary streams beside the layer kernel, forked from and
+ * joined back into the caller's stream by events (graph-capture safe). Part 0 (the longest rows,
+ * whose walk is a layer's critical path) goes to aux_streams[0] — create it with a high
+ * priority — part 1 to [1], the chain rows to [2]; with fewer streams the later parts share the
+ * last one (a budget for GPU_MAX_HW_QUEUES with RCCL running). lgcn_sched_create allocates the
+ * events (the only allocating call; once per stream set); NULL sched = everything in order on
+ * the caller's stream. */
+typedef struct lgcn_sched lgcn_sched_t;
+int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** out);
+int lgcn_sched_destroy(lgcn_sched_t* sched);
+#define LGCN_SCHED_SLOTS0        1  /* walk LDS slots of part 0 (0..LGCN_EMU_MAX_WALK_SLOTS) */
+#define LGCN_SCHED_SLOTS1        2  /* ... of part 1 (and of chain rows walked for lack of chains) */
+#define LGCN_SCHED_CHAIN         3  /* 0: walk the chain rows too (A/B, tests) */
+#define LGCN_SCHED_TIMING_START  4  /* hipEvent_t (or 0) recorded on the caller's stream right */
+#define LGCN_SCHED_TIMING_END    5  /* before / after the layer kernel of every layer (timing) */
+#define LGCN_SCHED_TRACE         6  /* hipEvent_t[8] (or 0): per-layer phase events — fork, part 0
+                                       and part 1 block passes done, layer kernel done, chains
+                                       done, part 0 and part 1 walks done, joined */
+int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
+
+/* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +
+ * chunk combine, the emulation block pass + walk of the emulated parts, the chain rows — every
+ * row of Y written once; concurrently under `sched` (above), else in order on `stream`. */
 int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
                int32_t n_rows, const lgcn_hub_plan_t* plan, lgcn_rows_t x, float x_div,
                const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
-               const lgcn_epilogue_t* epi_host, void* stream);
+               const lgcn_epilogue_t* epi_host, const lgcn_sched_t* sched, void* stream);
 
 /* Whole forward in one call: E1..E_{K-1} into layer_bufs_host[0..K-2] (each [n x d], ld = d),
  * final = mean(E0..EK) into out [n x d]. emb = E0 segments. plan: as in lgcn_layer (its
  * scratch sized for d). ev_host: NULL or 2*K hipEvent_t recorded around each layer (timing
- * only). */
+ * only). sched: as in lgcn_layer. */
 int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
                            const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                            lgcn_rows_t emb, int32_t d,
                            int32_t K, float* const* layer_bufs_host, float* out,
-                           void* const* ev_host, void* stream);
+                           void* const* ev_host, const lgcn_sched_t* sched, void* stream);
 
 /* Whole backward: grad_e0 = sum_k (Âᵀ)^k G/(K+1) in the Horner order autograd uses
  * (c = G/(K+1); h = c; K times h = c + Âᵀ h). rowptr/edges must be Âᵀ (== Â when symmetric)
  * and plan its hub plan. G is read in place as segments (the user/item/brand output grads); c
  * is never stored. grad_nz: NULL, or G's row bitmask (lgcn_rows_nonzero): a BPR batch touches
  * a few thousand rows, so the first layer gathers only those and no epilogue reads G's zero
- * rows. work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. */
+ * rows. work_h: [n x d] scratch (K > 1); grad_e0: [n x d], ld = d. sched: as in lgcn_layer. */
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             const int32_t* row_ids, int32_t n, const lgcn_hub_plan_t* plan,
                             lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
-                            float* grad_e0, void* stream);
+                            float* grad_e0, const lgcn_sched_t* sched, void* stream);
 
 /* ---- training batch loss (main.py:366-402) -------------------------------------------------- */
 /* Fused BPR + L2 loss of one batch of B gathered rows (u, p, n = final user / positive /

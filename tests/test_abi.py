@@ -71,14 +71,26 @@ def test_argument_validation_without_gpu(lib):
     assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 64, None, None, None) == -1
     assert lib.lgcn_rows_nonzero(engine.RowsT(), 10, 0, None, None, None) == -1
     assert lib.lgcn_propagate_forward(None, None, None, 5, None, rows, 64, -1,
-                                      None, None, None, None) == -1
+                                      None, None, None, None, None) == -1
     plan = engine.PlanT()
     plan.n_emu_rows = 3  # emulated rows without their buffers
     ep.mode = engine.LGCN_EPI_STORE
     assert lib.lgcn_layer(None, None, None, 0, ctypes.byref(plan), rows, 1.0, None, None, 64, 64,
-                          ctypes.byref(ep), None) == -1
+                          ctypes.byref(ep), None, None) == -1
     assert lib.lgcn_layer(None, None, None, 0, None, rows, 1.0, None, None, 64, 64,
-                          ctypes.byref(ep), None) == -1
+                          ctypes.byref(ep), None, None) == -1
+    plan.n_emu_rows, plan.n_emu_blocks = 0, 0
+    plan.emu_part_rows[0], plan.emu_part_rows[1] = 1, 0  # parts out of order
+    assert lib.lgcn_layer(None, None, None, 0, ctypes.byref(plan), rows, 1.0, None, None, 64, 64,
+                          ctypes.byref(ep), None, None) == -1
+    # the schedule: 1..3 auxiliary streams; its knobs validated before any HIP call
+    h = ctypes.c_void_p()
+    assert lib.lgcn_sched_create(None, 2, ctypes.byref(h)) == -1
+    arr = (ctypes.c_void_p * 4)()
+    assert lib.lgcn_sched_create(arr, 4, ctypes.byref(h)) == -1
+    assert lib.lgcn_sched_create(arr, 0, ctypes.byref(h)) == -1
+    assert lib.lgcn_sched_set(None, engine.SCHED_SLOTS0, 4) == -1
+    assert lib.lgcn_sched_destroy(None) == 0
     assert lib.lgcn_emu_blocks(None, None, -1, rows, 1.0, None, 64, None, None, None, None) == -1
     assert lib.lgcn_emu_blocks(None, None, 0, rows, 1.0, None, 64, None, None, None, None) == 0
     assert lib.lgcn_emu_walk(None, None, None, 2, None, None, None, rows, 1.0, None, None, 64, 64,
@@ -91,7 +103,7 @@ def test_argument_validation_without_gpu(lib):
                                None) == 0     # nothing to do
     assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 24, ctypes.byref(ep),
                                None) == -1    # unsupported width
-    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 0
+    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4  # (+ tail padding)
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
                                   ctypes.byref(nbytes), None) == -1

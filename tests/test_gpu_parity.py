@@ -254,16 +254,22 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
         assert hp.n_pre > 0
     if mode == "exact":
         assert hp.n_emu_rows > 0 and hp.n_long > 0
-    plan = hp.struct(d, gpu_device)
+    # the plan with its walk/chain parts, and the concurrent schedule over auxiliary streams (the
+    # same lgcn_layer schedule engine.spmm_layer runs); then again in order on one stream
+    plan = hp.struct(d, gpu_device, nnz=g.nnz)
+    sched = engine.sched_for(gpu_device)
+    assert sched is not None and sched.n_aux == 3
     layers = [torch.empty((n, d), device=gpu_device) for _ in range(K - 1)]
     out = torch.empty((n, d), device=gpu_device)
     bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
-    rc = lib.lgcn_propagate_forward(P(g.rowptr), P(g.edges), P(g.row_ids), n, ctypes.byref(plan),
-                                    engine.rows_desc(segs, d), d, K,
-                                    ctypes.cast(bufs, ctypes.c_void_p), P(out), None, st)
-    assert rc == 0
     want = engine.propagate_forward(g, segs, K, thr, hub_mode=kw["mode"], emu_min=48)
-    assert torch.equal(out, want)
+    for sc in (sched.handle, None):
+        out.fill_(float("nan"))
+        rc = lib.lgcn_propagate_forward(P(g.rowptr), P(g.edges), P(g.row_ids), n,
+                                        ctypes.byref(plan), engine.rows_desc(segs, d), d, K,
+                                        ctypes.cast(bufs, ctypes.c_void_p), P(out), None, sc, st)
+        assert rc == 0
+        assert torch.equal(out, want)
     ref = oracle.forward(z["adj_row"], z["adj_col"], z["adj_val"], case_e0(z), K)
     if mode != "chunk":
         assert np.array_equal(out.cpu().numpy(), ref)
@@ -271,15 +277,18 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
         assert_close_normwise(out.cpu().numpy(), ref, what="two-level combine")
     G = torch.from_numpy(upstream_grad(n, d)).to(gpu_device)
     gt = g.transpose
-    plan_t = gt.hubs(thr, **kw).struct(d, gpu_device)
+    plan_t = gt.hubs(thr, **kw).struct(d, gpu_device, nnz=gt.nnz)
     work = torch.empty((n, d), device=gpu_device)
     ge0 = torch.empty((n, d), device=gpu_device)
-    rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n,
-                                     ctypes.byref(plan_t), engine.rows_desc([G], d), None, d, K,
-                                     P(work), P(ge0), st)
-    assert rc == 0
     bkw = dict(sparse="off", hub_mode=kw["mode"], emu_min=48)
-    assert torch.equal(ge0, engine.propagate_backward(g, [G], K, thr, **bkw))
+    want_b = engine.propagate_backward(g, [G], K, thr, **bkw)
+    for sc in (sched.handle, None):
+        ge0.fill_(float("nan"))
+        rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n,
+                                         ctypes.byref(plan_t), engine.rows_desc([G], d), None, d,
+                                         K, P(work), P(ge0), sc, st)
+        assert rc == 0
+        assert torch.equal(ge0, want_b)
     if mode != "chunk":
         assert np.array_equal(ge0.cpu().numpy(), oracle.backward(
             z["adj_row"], z["adj_col"], z["adj_val"], upstream_grad(n, d), K))
@@ -290,7 +299,7 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
     nz, _ = engine.rows_nonzero([Gs], d, gpu_device)
     rc = lib.lgcn_propagate_backward(P(gt.rowptr), P(gt.edges), P(gt.row_ids), n,
                                      ctypes.byref(plan_t), engine.rows_desc([Gs], d), P(nz), d, K,
-                                     P(work), P(ge0), st)
+                                     P(work), P(ge0), sched.handle, st)
     assert rc == 0
     assert torch.equal(ge0, engine.propagate_backward(g, [Gs], K, thr, **bkw))
 

@@ -34,7 +34,7 @@ def timed(fn, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--emu-min", default="4096,32768,131072,524288")
+    ap.add_argument("--emu-min", default="0")
     ap.add_argument("--layers", type=int, default=2)
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
@@ -58,7 +58,9 @@ def main():
         hp = g.hubs(128, mode="exact", emu_min=emu_min)
         plan = hp.struct(d, dev)
         rest = engine.PlanT.from_buffer_copy(plan)
-        rest.n_emu_rows = rest.n_emu_blocks = 0
+        rest.n_emu_rows = rest.n_emu_blocks = rest.emu_scratch_blocks = 0
+        rest.emu_part_rows[0] = rest.emu_part_rows[1] = 0
+        rest.emu_part_blocks[0] = rest.emu_part_blocks[1] = 0
         args = (P(g.rowptr), P(g.edges), P(g.row_ids), g.n_rows)
         print(f"emu_min {emu_min}: long rows {hp.n_long}, emulated rows {hp.n_emu_rows} "
               f"({hp.n_emu_blocks} blocks, {int(deg[:hp.n_emu_rows].sum()):,} edges)", flush=True)
@@ -68,23 +70,41 @@ def main():
             t = {}
             t["layer_kernel"] = timed(lambda: lib.lgcn_layer(*args, ctypes.byref(rest), x, 1.0,
                                                              None, P(y), d, d, ctypes.byref(ep),
-                                                             st))
+                                                             None, st))
             if hp.n_emu_rows:
-                def blocks():
-                    assert lib.lgcn_emu_blocks(P(g.edges), plan.emu_blocks, hp.n_emu_blocks, x,
-                                               1.0, None, d, plan.emu_rel, plan.emu_meta,
-                                               plan.emu_stage, st) == 0
-                t["block_pass"] = timed(blocks)
+                (r0, r1), (b0, b1) = hp.walk_parts(g.nnz)
+                nb_all = hp.n_emu_blocks
 
-                def walk(lo, hi):
+                def blocks(k0, k1):
+                    assert lib.lgcn_emu_blocks(
+                        P(g.edges), plan.emu_blocks + k0 * 16, k1 - k0, x, 1.0, None, d,
+                        plan.emu_rel + k0 * d * engine.LGCN_EMU_CANDS * 4,
+                        plan.emu_meta + k0 * d * engine.LGCN_EMU_META_BYTES,
+                        plan.emu_stage + k0 * (d + 1) * engine.LGCN_EMU_BLOCK * 4, st) == 0
+                t["part0_blocks"] = timed(lambda: blocks(0, b0))
+                t["part1_blocks"] = timed(lambda: blocks(b0, b1))
+                t["blocks_all_walked"] = timed(lambda: blocks(0, b1))
+                slots = engine.emu_slots()
+
+                def walk(lo, hi, sl):
                     assert lib.lgcn_emu_walk(P(g.edges), plan.emu_blocks,
                                              hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
                                              plan.emu_meta, plan.emu_stage, x, 1.0, None, P(y),
-                                             d, d, ctypes.byref(ep), 0, st) == 0
-                t["walk_all"] = timed(lambda: walk(0, hp.n_emu_rows))
-                t["walk_row0"] = timed(lambda: walk(0, 1))
-                if hp.n_emu_rows > 1:
-                    t["walk_rows_1+"] = timed(lambda: walk(1, hp.n_emu_rows))
+                                             d, d, ctypes.byref(ep), sl, st) == 0
+                blocks(0, b1)
+                t["walk_row0"] = timed(lambda: walk(0, 1, slots[0]))
+                if r0 > 0:
+                    t["walk_part0"] = timed(lambda: walk(0, r0, slots[0]))
+                if r1 > r0:
+                    t["walk_part1"] = timed(lambda: walk(r0, r1, slots[-1]))
+                if hp.n_emu_rows > r1:
+                    rb = hp.emu_rows.element_size() * 4
+                    t["chain_rows"] = timed(lambda: lib.lgcn_chain_rows(
+                        P(g.edges), plan.emu_blocks, plan.emu_rows + r1 * rb, hp.n_emu_rows - r1,
+                        x, 1.0, P(y), d, d, ctypes.byref(ep), st))
+                print(f"  parts: rows {r0}/{r1 - r0}/{hp.n_emu_rows - r1} (walk part 0 / walk "
+                      f"part 1 / chain), walked blocks {b1} of {nb_all}; chain max degree "
+                      f"{engine.chain_max_degree(g.nnz)}", flush=True)
             t["layer_overlapped"] = timed(lambda: engine.spmm_layer(g, xs, y, d, ep, 128, hp))
             os.environ["LGCN_EMU_OVERLAP"] = "0"
             t["layer_serial"] = timed(lambda: engine.spmm_layer(g, xs, y, d, ep, 128, hp))

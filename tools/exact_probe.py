@@ -162,7 +162,7 @@ def walk_timing(g, segs, d, thr, emu_min):
             assert lib.lgcn_emu_walk(engine._ptr(g.edges), plan.emu_blocks,
                                      hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
                                      plan.emu_meta, plan.emu_stage, x, 1.0, None, engine._ptr(y),
-                                     d, d, ctypes.byref(ep), 0, st) == 0
+                                     d, d, ctypes.byref(ep), engine.emu_slots()[0], st) == 0
             b.record()
             torch.cuda.synchronize()
             print(f"  walk rows [{lo}, {hi}): {a.elapsed_time(b):.3f} ms", flush=True)
