@@ -17,6 +17,13 @@ import os
 import sys
 import time
 
+# The bipartite two-lane schedule runs 8 streams (lgcn_sched_create: the caller's + 7); every
+# stream wants a hardware queue of its own, and HIP reads this once, when the process first
+# touches the GPU (its default, 4, makes the lanes share queues: same bits, less overlap).
+# LGCN_HW_QUEUES=keep leaves the environment's value alone.
+if os.environ.get("LGCN_HW_QUEUES", "") != "keep":
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LGCN_HW_QUEUES", "") or "8"
+
 import numpy as np
 import torch
 
@@ -359,7 +366,10 @@ def main():
     idx = torch.from_numpy(np.vstack((r, c)))
     adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v), (n, n)).to(dev)
     del idx
-    g = engine.graph_from_coo(adj)
+    # the sides the model offers (engine.propagate_blocks: the item rows): a bipartite graph is
+    # stored side-major and propagated by the two-lane schedule
+    g = engine.graph_from_coo(adj, sides=(U, U + I))
+    sided = g.split is not None
     hp = g.hubs(hub_thr)
     torch.cuda.synchronize()
     prep_s = time.time() - t0
@@ -421,7 +431,9 @@ def main():
                                             kernel_events=kev, hub_mode=mode)
 
     def timed(mode, steps, warmup):
-        """(ms per step, [steps x K] layer ms, [steps x K] layer-kernel ms, output)"""
+        """(ms per step, [steps x K] layer ms, [steps x K] layer-kernel ms, output). Sided: no
+        layer boundary exists (the two lanes overlap layers), layer ms is None and the kernel ms
+        are [steps x K x 2] — each half-layer's layer kernel, timed on its lane's stream."""
         for _ in range(warmup):
             step(mode=mode)
         torch.cuda.synchronize()
@@ -429,15 +441,34 @@ def main():
         evs = [[mk() for _ in range(K)] for _ in range(steps)]
         kevs = [[mk() for _ in range(K)] for _ in range(steps)]
         a_, b_ = mk()
+        if sided:
+            engine.side_timing = []
         torch.cuda.synchronize()
         a_.record()
         for s_ in range(steps):
-            o = step(evs[s_], kevs[s_], mode)
+            o = step(None, None, mode) if sided else step(evs[s_], kevs[s_], mode)
         b_.record()
         torch.cuda.synchronize()
+        if sided:
+            tm, engine.side_timing = engine.side_timing, None
+            ker = np.array([[[t[(k, s)][0].elapsed_time(t[(k, s)][1]) for s in (0, 1)]
+                             for k in range(1, K + 1)] for t in tm])
+            return a_.elapsed_time(b_) / steps, None, ker, o
         lay = np.array([[x.elapsed_time(y) for x, y in st] for st in evs])
         ker = np.array([[x.elapsed_time(y) for x, y in st] for st in kevs])
         return a_.elapsed_time(b_) / steps, lay, ker, o
+
+    def side_phases(fn):
+        """Per-half-layer phase log of one call of fn (ms from its first fork): the lanes'
+        critical paths, engine.side_trace."""
+        engine.side_trace = []
+        fn()
+        torch.cuda.synchronize()
+        tr, engine.side_trace = engine.side_trace[0], None
+        t0_ = tr[(1, 0)][0][1]
+        return {f"layer{k}_side{s}_lane{(k + s) % 2}":
+                {nm: round(t0_.elapsed_time(ev), 3) for nm, ev in tr[(k, s)][1:]}
+                for (k, s) in sorted(tr)}
 
     # the headline: the engine's default (exact) hub mode — every row bitwise the reference's
     hub_mode = engine.hub_mode_from_env()
@@ -454,31 +485,50 @@ def main():
     # frac = MEASURED HBM bytes per launch (profiles/traffic_<config>_<gen>.json: rocprofv3 PMC
     # FETCH_SIZE + WRITE_SIZE, stamped with the hash of the kernel sources; a stale file is
     # refused) / launch time / peak. Algorithmic bytes are reported beside it.
-    b_layer = nnz * (4 * d + 8) + 4 * (n + 1) + 4 * n * d
-    store_ms = float(kern_ms[:, :-1].mean()) if K > 1 else float(kern_ms.mean())
-    mean_ms = float(kern_ms[:, -1].mean())
-    layer_avg = float(layer_ms.mean())
+    # algorithmic bytes of one layer-kernel launch (SURVEY §8d per-edge model over the rows the
+    # kernel itself runs — bundle rows, degree <= threshold; hub rows run beside it): gathered
+    # X rows (4d) + edge records (8) per edge, row pointers, one written row per bundle row
+    rp_h = g.rowptr_host().astype(np.int64)
+
+    def kernel_bytes(s0, s1):
+        deg_ = np.diff(rp_h[s0:s1 + 1])
+        bun = deg_ <= min(hub_thr, engine.INT32_MAX)
+        return int(deg_[bun].sum()) * (4 * d + 8) + 4 * (s1 - s0 + 1) + 4 * int(bun.sum()) * d
+    if sided:
+        b_side = [kernel_bytes(0, g.split), kernel_bytes(g.split, n)]
+        b_layer = sum(b_side) / 2          # per launch, averaged over the two sides' launches
+        store_ms = float(kern_ms[:, :-1, :].mean()) if K > 1 else float(kern_ms.mean())
+        mean_ms = float(kern_ms[:, -1, :].mean())
+        kname = (f"k_layer<float4,{min(64, d // 4)},{max(1, d // 256)},STORE> half-layer launches "
+                 f"(layers 1..K-1, both sides: bundle rows of the users / items)")
+    else:
+        b_layer = kernel_bytes(0, n)
+        store_ms = float(kern_ms[:, :-1].mean()) if K > 1 else float(kern_ms.mean())
+        mean_ms = float(kern_ms[:, -1].mean())
+        kname = (f"k_layer<float4,{min(64, d // 4)},{max(1, d // 256)},STORE> "
+                 f"(layers 1..K-1: bundle rows)")
     alg = b_layer / (store_ms / 1e3) / 1e9
     roof = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": None, "traffic": None,
-            "kernel": f"k_layer<float4,{min(64, d // 4)},{max(1, d // 256)},STORE> "
-                      f"(layers 1..K-1: bundles + whole long rows)",
+            "frac": None, "traffic": None, "kernel": kname,
             "avg_launch_ms": round(store_ms, 4),
-            "algorithmic": {"bytes_per_launch": b_layer, "achieved": round(alg, 1),
+            "algorithmic": {"bytes_per_launch": int(b_layer), "achieved": round(alg, 1),
                             "frac": round(alg / PEAK_HBM_GBS, 4),
-                            "note": "SURVEY §8d byte model; above the measured rate when hot "
-                                    "gathered rows hit L2/MALL"},
-            "layer": {"avg_ms": round(layer_avg, 4),
-                      "per_layer_ms": [round(x, 4) for x in layer_ms.mean(0).tolist()],
-                      "per_layer_kernel_ms": [round(x, 4) for x in kern_ms.mean(0).tolist()],
-                      "algorithmic_frac": round(b_layer / (layer_avg / 1e3) / 1e9
-                                                / PEAK_HBM_GBS, 4),
-                      "note": "whole layer = layer kernel + the exact emulation of the hub rows "
-                              "(block pass + walk on side streams): the walk of the 2.77M-edge "
-                              "row is a latency-bound chain, not an HBM-bound stream; the STORE "
-                              "kernel's time (and so frac) is measured as it runs, sharing the "
-                              "GPU with the emulation kernels"},
+                            "note": "SURVEY §8d byte model over the kernel's own rows; above the "
+                                    "measured rate when hot gathered rows hit L2/MALL"},
             "mean_layer": {"avg_launch_ms": round(mean_ms, 4)}}
+    if sided:
+        roof["half_layer_kernel_ms"] = {f"layer{k + 1}": [round(float(x), 4) for x in row]
+                                        for k, row in enumerate(kern_ms.mean(0))}
+        roof["algorithmic"]["bytes_per_side"] = b_side
+        roof["note"] = ("the layer kernel's time (and so frac) is measured as it runs, sharing "
+                        "the GPU with the emulation kernels and the other lane")
+    else:
+        layer_avg = float(layer_ms.mean())
+        roof["layer"] = {"avg_ms": round(layer_avg, 4),
+                         "per_layer_ms": [round(x, 4) for x in layer_ms.mean(0).tolist()],
+                         "per_layer_kernel_ms": [round(x, 4) for x in kern_ms.mean(0).tolist()],
+                         "note": "whole layer = layer kernel + the exact emulation of the hub "
+                                 "rows (block pass + walk on side streams)"}
     def attach_traffic(roof, mode, store_ms):
         """frac from the committed PMC traffic of this kernel-source build (refused if stale)."""
         suffix = "" if mode == "exact" else f"_{mode}"
@@ -511,6 +561,9 @@ def main():
                    "brands": B, "content_dim": fusion,
                    "hub_threshold": hub_thr, "hub_mode": hub_mode,
                    "emu_min_degree": engine.emu_min_degree_from_env(),
+                   "schedule": ("bipartite two-lane (lgcn_propagate_forward_sides), "
+                                f"{engine.n_aux_streams()} aux streams, GPU_MAX_HW_QUEUES="
+                                f"{engine.hw_queues()}") if sided else "one operator",
                    "parallelism": "single"},
         "roofline": roof,
         "wall_s_timed": round(wall, 3), "prep_s": round(prep_s, 2),
@@ -518,6 +571,11 @@ def main():
     }
     if fusion:
         result["fusion_prelayer"] = prelayer
+    if sided:
+        result["phases_ms"] = {"forward": side_phases(lambda: step(mode=hub_mode)),
+                               "note": "one forward's half-layers (layer k, side s on lane "
+                                       "(k+s)%2; side 0 = users(+brands), 1 = items): ms from "
+                                       "the first fork at which each part is done"}
 
     # BASELINE configs[3] on the same graph (d=256, K=4): the 1-GPU side of the 8-GPU target
     # (dist.featsplit_c4 times the same forward on d/P columns per rank at N > 1)
@@ -527,30 +585,21 @@ def main():
         x4 = (torch.rand((n, D.C4_D), generator=gen4, device=dev) * 2 - 1) * float(
             np.sqrt(6.0 / (n + D.C4_D)))
         c4 = {"d": D.C4_D, "layers": D.C4_K}
-        b4 = nnz * (4 * D.C4_D + 8) + 4 * (n + 1) + 4 * n * D.C4_D
+        x4s = [x4[:U], x4[U:]]   # the model's segments: the sided schedule when g has sides
         for mode in ("exact", "chunk"):
             for _ in range(2):
-                engine.propagate_forward(g, [x4], D.C4_K, hub_thr, hub_mode=mode)
+                engine.propagate_forward(g, x4s, D.C4_K, hub_thr, hub_mode=mode)
             mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev4 = [[mk() for _ in range(D.C4_K)] for _ in range(5)]
-            kv4 = [[mk() for _ in range(D.C4_K)] for _ in range(5)]
             a4, z4 = mk()
             torch.cuda.synchronize()
             a4.record()
             for s_ in range(5):
-                engine.propagate_forward(g, [x4], D.C4_K, hub_thr, layer_events=ev4[s_],
-                                         kernel_events=kv4[s_], hub_mode=mode)
+                engine.propagate_forward(g, x4s, D.C4_K, hub_thr, hub_mode=mode)
             z4.record()
             torch.cuda.synchronize()
             ms4 = a4.elapsed_time(z4) / 5
-            lay4 = np.array([[a.elapsed_time(b) for a, b in st] for st in ev4]).mean(0)
-            ker4 = np.array([[a.elapsed_time(b) for a, b in st] for st in kv4]).mean(0)
             c4[mode] = {"ms_per_step": round(ms4, 3),
-                        "edges_per_s": round(D.C4_K * nnz / (ms4 / 1e3), 1),
-                        "per_layer_ms": [round(float(x), 3) for x in lay4],
-                        "store_kernel_ms": round(float(ker4[:-1].mean()), 3),
-                        "store_kernel_algorithmic_frac": round(
-                            b4 / (ker4[:-1].mean() / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
+                        "edges_per_s": round(D.C4_K * nnz / (ms4 / 1e3), 1)}
         result["c4_same_graph"] = c4
         del x4
         torch.cuda.empty_cache()
@@ -650,11 +699,13 @@ def main():
         store_c = float(ker_c[:, :-1].mean())
         roof_c = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                   "frac": None, "traffic": None, "avg_launch_ms": round(store_c, 4),
-                  "algorithmic_frac": round(b_layer / (store_c / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
+                  "note": "chunk items run inside the layer kernel: more bytes than the "
+                          "exact-mode byte model counts"}
         attach_traffic(roof_c, "chunk", store_c)
         result["chunk_mode"] = {
             "ms_per_step": round(ms_c, 4), "edges_per_s": round(K * nnz / (ms_c / 1e3), 1),
-            "per_layer_ms": [round(x, 4) for x in lay_c.mean(0).tolist()],
+            "per_layer_ms": ([round(x, 4) for x in lay_c.mean(0).tolist()]
+                             if lay_c is not None else None),
             "store_kernel_ms": round(store_c, 4), "roofline": roof_c,
             "parity": pc,
             "what": "hub_mode=chunk: rows above hub_threshold cut into fixed chunks summed in a "

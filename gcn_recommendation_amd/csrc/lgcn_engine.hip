@@ -108,12 +108,40 @@ __global__ void k_csr_symmetric(const int32_t* __restrict__ rowptr,
 // Processing order: slots sorted by degree (descending, stable). The lane groups of a wave then
 // stream rows of equal length (no group idles while a longer neighbour finishes) and hub rows
 // come first. Each row keeps its own edge order, so every output row is the same fp32 chain.
-__global__ void k_csr_degrees(const int32_t* __restrict__ rowptr, int32_t n,
-                              int32_t* __restrict__ deg, int32_t* __restrict__ iota) {
+// side_bit: set on the rows outside [lo, hi) (sorted descending, they take the first slots)
+__device__ __forceinline__ int32_t side_flag(int64_t r, int32_t lo, int32_t hi, int32_t side_bit) {
+    return (r >= lo && r < hi) ? 0 : side_bit;
+}
+
+__global__ void k_csr_degrees(const int32_t* __restrict__ rowptr, int32_t n, int32_t lo,
+                              int32_t hi, int32_t side_bit, int32_t* __restrict__ deg,
+                              int32_t* __restrict__ iota) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    deg[r] = rowptr[r + 1] - rowptr[r];
+    deg[r] = (rowptr[r + 1] - rowptr[r]) | side_flag(r, lo, hi, side_bit);
     iota[r] = (int32_t)r;
+}
+
+__global__ void k_csr_mask_degrees(int32_t* __restrict__ deg, int32_t n, int32_t mask) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) deg[s] &= mask;
+}
+
+// bad |= some edge joins two rows on the same side of [lo, hi) (row of edge j by binary search)
+__global__ void k_csr_bipartite(const int32_t* __restrict__ rowptr,
+                                const lgcn_edge_t* __restrict__ edges,
+                                const int32_t* __restrict__ row_ids, int32_t n_rows, int64_t nnz,
+                                int32_t lo, int32_t hi, int32_t* bad) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    int32_t a = 0, b = n_rows - 1;
+    while (a < b) {
+        const int32_t mid = (a + b + 1) >> 1;
+        if (rowptr[mid] <= j) a = mid; else b = mid - 1;
+    }
+    const int32_t r = row_ids ? row_ids[a] : a;
+    const int32_t c = load_edge(edges + j).x;
+    if ((r >= lo && r < hi) == (c >= lo && c < hi)) atomicOr(bad, 1);
 }
 
 // rank[row_ids[s]] = s: position of every row in the degree-descending order
@@ -131,7 +159,8 @@ __global__ void k_csr_rank(const int32_t* __restrict__ row_ids, int32_t n, int32
 constexpr int32_t kKeyMaxDeg = 256;
 __global__ void k_csr_degree_key(const int32_t* __restrict__ rowptr,
                                  const lgcn_edge_t* __restrict__ edges, int32_t n,
-                                 const int32_t* __restrict__ rank, uint64_t* __restrict__ comp,
+                                 const int32_t* __restrict__ rank, int32_t lo, int32_t hi,
+                                 int32_t side_bit, uint64_t* __restrict__ comp,
                                  int32_t* __restrict__ iota) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -142,16 +171,17 @@ __global__ void k_csr_degree_key(const int32_t* __restrict__ rowptr,
             const uint32_t k = (uint32_t)rank[(int32_t)edges[j]] + 1u;
             key = k > key ? k : key;
         }
-    comp[r] = ((uint64_t)(uint32_t)(e - b) << 32) | (uint64_t)(0xFFFFFFFFu - key);
+    comp[r] = ((uint64_t)(uint32_t)((e - b) | side_flag(r, lo, hi, side_bit)) << 32) |
+              (uint64_t)(0xFFFFFFFFu - key);
     iota[r] = (int32_t)r;
 }
 
 __global__ void k_csr_slot_degrees(const int32_t* __restrict__ row_ids,
-                                   const int32_t* __restrict__ deg, int32_t n,
+                                   const int32_t* __restrict__ deg, int32_t n, int32_t mask,
                                    int32_t* __restrict__ deg_sorted) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
-    deg_sorted[s] = deg[row_ids[s]];
+    deg_sorted[s] = deg[row_ids[s]] & mask;
 }
 
 // edges_out[j] = the edge record of slot s (binary search: rowptr_out[s] <= j < rowptr_out[s+1])
@@ -468,27 +498,35 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
 }
 
 int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
-                             int64_t nnz, int32_t* deg_tmp, int32_t* deg_sorted, int32_t* iota_tmp,
+                             int64_t nnz, int32_t side_lo, int32_t side_hi, int32_t* deg_tmp,
+                             int32_t* deg_sorted, int32_t* iota_tmp,
                              int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
                              uint64_t* key_tmp, uint64_t* key_sorted,
                              void* temp, size_t* temp_bytes_host, void* stream) {
     if (n_rows < 0 || nnz < 0 || nnz > 0x7fffffffLL || !temp_bytes_host) return LGCN_EINVAL;
     if ((key_tmp == nullptr) != (key_sorted == nullptr)) return LGCN_EINVAL;
+    if (side_lo < 0 || side_lo > side_hi || side_hi > n_rows) return LGCN_EINVAL;
     int end_bit = 1;  // degrees are <= nnz
     while (end_bit < 31 && (1LL << end_bit) <= nnz) ++end_bit;
+    // sides: one more key bit above the degree, set on the rows outside [side_lo, side_hi)
+    const bool sided = side_lo < side_hi;
+    if (sided && end_bit > 30) return LGCN_EINVAL;  // (2^30 nonzeros)
+    const int32_t side_bit = sided ? (int32_t)(1u << end_bit) : 0;
+    const int32_t deg_mask = sided ? side_bit - 1 : -1;
+    const int sort_bits = end_bit + (sided ? 1 : 0);
     hipStream_t s = S(stream);
     const int n = n_rows;
     const bool keyed = key_tmp != nullptr;
     if (temp == nullptr) {
         size_t b1 = 0, b2 = 0, b3 = 0;
         hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(
-            nullptr, b1, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, end_bit, s);
+            nullptr, b1, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, sort_bits, s);
         if (e != hipSuccess) return (int)e;
         e = hipcub::DeviceScan::InclusiveSum(nullptr, b2, deg_sorted, rowptr_out, n, s);
         if (e != hipSuccess) return (int)e;
         if (keyed) {
             e = hipcub::DeviceRadixSort::SortPairsDescending(
-                nullptr, b3, key_tmp, key_sorted, iota_tmp, row_ids, n, 0, 32 + end_bit, s);
+                nullptr, b3, key_tmp, key_sorted, iota_tmp, row_ids, n, 0, 32 + sort_bits, s);
             if (e != hipSuccess) return (int)e;
         }
         size_t b = b1 > b2 ? b1 : b2;
@@ -501,26 +539,30 @@ int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, in
     if (int e = herr(hipMemsetAsync(rowptr_out, 0, sizeof(int32_t), s))) return e;
     if (n == 0) return 0;
     const dim3 gn((uint32_t)((n + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL(k_csr_degrees, gn, dim3(kBlock), 0, s, rowptr, n, deg_tmp, iota_tmp);
+    hipLaunchKernelGGL(k_csr_degrees, gn, dim3(kBlock), 0, s, rowptr, n, side_lo, side_hi,
+                       side_bit, deg_tmp, iota_tmp);
     if (int e = last_err()) return e;
     size_t bytes = *temp_bytes_host;
     // LSD radix sort: stable, so rows of equal degree keep their id order
     if (int e = herr(hipcub::DeviceRadixSort::SortPairsDescending(
-            temp, bytes, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, end_bit, s)))
+            temp, bytes, deg_tmp, deg_sorted, iota_tmp, row_ids, n, 0, sort_bits, s)))
         return e;
-    if (keyed) {  // second, stable sort by (degree, neighbour key); the permutation only
+    if (keyed) {  // second, stable sort by (side, degree, neighbour key); the permutation only
         // reorders work and slots, every row keeps its edges (bitwise-neutral)
         hipLaunchKernelGGL(k_csr_rank, gn, dim3(kBlock), 0, s, row_ids, n, deg_sorted);
         if (int e = last_err()) return e;
         hipLaunchKernelGGL(k_csr_degree_key, gn, dim3(kBlock), 0, s, rowptr, edges, n, deg_sorted,
-                           key_tmp, iota_tmp);
+                           side_lo, side_hi, side_bit, key_tmp, iota_tmp);
         if (int e = last_err()) return e;
         bytes = *temp_bytes_host;
         if (int e = herr(hipcub::DeviceRadixSort::SortPairsDescending(
-                temp, bytes, key_tmp, key_sorted, iota_tmp, row_ids, n, 0, 32 + end_bit, s)))
+                temp, bytes, key_tmp, key_sorted, iota_tmp, row_ids, n, 0, 32 + sort_bits, s)))
             return e;
         hipLaunchKernelGGL(k_csr_slot_degrees, gn, dim3(kBlock), 0, s, row_ids, deg_tmp, n,
-                           deg_sorted);
+                           deg_mask, deg_sorted);
+        if (int e = last_err()) return e;
+    } else if (sided) {
+        hipLaunchKernelGGL(k_csr_mask_degrees, gn, dim3(kBlock), 0, s, deg_sorted, n, deg_mask);
         if (int e = last_err()) return e;
     }
     bytes = *temp_bytes_host;
@@ -529,6 +571,19 @@ int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, in
     if (nnz == 0) return 0;
     hipLaunchKernelGGL(k_csr_gather_rows, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, s, rowptr_out, row_ids, rowptr, edges, n, nnz, edges_out);
+    return last_err();
+}
+
+int lgcn_csr_check_bipartite(const int32_t* rowptr, const lgcn_edge_t* edges,
+                             const int32_t* row_ids, int32_t n_rows, int64_t nnz,
+                             int32_t side_lo, int32_t side_hi, int32_t* bad, void* stream) {
+    if (n_rows < 0 || nnz < 0 || !bad || side_lo < 0 || side_lo > side_hi || side_hi > n_rows)
+        return LGCN_EINVAL;
+    if (nnz == 0) return 0;
+    if (!rowptr || !edges || n_rows == 0) return LGCN_EINVAL;
+    hipLaunchKernelGGL(k_csr_bipartite, dim3((uint32_t)((nnz + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, S(stream), rowptr, edges, row_ids, n_rows, nnz, side_lo,
+                       side_hi, bad);
     return last_err();
 }
 
@@ -658,6 +713,15 @@ struct lgcn_sched {
     int chain;              // 0: chain rows are walked too (tests / A-B)
     hipEvent_t t0, t1;      // optional: recorded on the caller's stream around the layer kernel
     hipEvent_t* trace;      // optional [8]: phase events (LGCN_SCHED_TRACE)
+    // bipartite lanes (lgcn_propagate_*_sides; created with >= 4 aux streams): the second lane's
+    // main stream and its own view (aux streams + fork/join events), the events that fork it
+    // from / join it into the caller's stream, and cross[side]: a side's layer K-1 done (the
+    // final mean half-layer of that side, on the other lane, waits for it)
+    hipStream_t lane1_main;
+    lgcn_sched* lane1;
+    hipEvent_t lane_fork, lane_join, cross[2];
+    hipEvent_t* trace_sides;  // optional [16 K] (LGCN_SCHED_TRACE_SIDES)
+    hipEvent_t* timing_sides; // optional [4 K] (LGCN_SCHED_TIMING_SIDES)
 };
 
 namespace {
@@ -782,6 +846,83 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     return mark(7, s);
 }
 
+// The bipartite schedule (lgcn_propagate_*_sides): a lane = the stream its half-layers' layer
+// kernels run on + the schedule view whose aux streams take their emulated / chain rows.
+struct Lane {
+    hipStream_t main;
+    const lgcn_sched* view;
+};
+
+// Half-layer (k, side): the rows of slots [0, split) (side 0) or [split, n) (side 1), under that
+// side's plan with scratch set k & 1, traced at trace_sides[((k - 1) * 2 + side) * 8].
+int half_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+               int32_t n, int32_t split, const lgcn_hub_plan_t* plans, int k, int side,
+               const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y, int32_t d,
+               const lgcn_epilogue_t& ep, const lgcn_sched* sc, const Lane& L) {
+    const int32_t s0 = side ? split : 0, s1 = side ? n : split;
+    if (s1 <= s0) return 0;
+    const int h = (k - 1) * 2 + side;
+    lgcn_sched v;
+    const lgcn_sched* vp = nullptr;
+    hipEvent_t* tm = sc ? sc->timing_sides : nullptr;
+    if (L.view) {
+        v = *L.view;
+        v.t0 = tm ? tm[2 * h] : nullptr;
+        v.t1 = tm ? tm[2 * h + 1] : nullptr;
+        v.trace = sc && sc->trace_sides ? sc->trace_sides + h * 8 : nullptr;
+        vp = &v;
+    }
+    return plan_layer(rowptr + s0, edges, row_ids + s0, s1 - s0, plans[2 * side + (k & 1)], x,
+                      xdiv, x_nz, y, d, d, ep, vp, L.main);
+}
+
+// The two lanes: lane 1 on its own streams when the schedule has them, else both lanes share
+// the caller's stream (half-layers then run in layer order, each still overlapped inside).
+bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2]) {
+    lanes[0] = Lane{s, sc};
+    const bool two = sc && sc->lane1;
+    lanes[1] = two ? Lane{sc->lane1_main, sc->lane1->n_aux ? sc->lane1 : nullptr} : lanes[0];
+    return two;
+}
+
+// Lane 1 forked from the caller's stream: its main stream AND its aux streams wait on `s` first
+// (a stream captured by way of another forked stream — origin -> A -> B — crashes HIP's
+// hipStreamEndCapture on this ROCm; every stream entering the capture from the origin is fine).
+int fork_lanes(const lgcn_sched* sc, bool two, hipStream_t s) {
+    if (!two) return 0;
+    if (int e = herr(hipEventRecord(sc->lane_fork, s))) return e;
+    if (int e = herr(hipStreamWaitEvent(sc->lane1_main, sc->lane_fork, 0))) return e;
+    const lgcn_sched* l1 = sc->lane1;
+    for (int i = 0; i < l1->n_aux; ++i)
+        if (int e = herr(hipStreamWaitEvent(l1->aux[i], sc->lane_fork, 0))) return e;
+    return 0;
+}
+
+// Lane 1 back into the caller's stream: its main stream and (already joined into that) its aux
+// streams, each also joined into `s` directly — a captured stream forked from another forked
+// stream must still end joined into the capture's origin for hipStreamEndCapture.
+int join_lanes(const lgcn_sched* sc, bool two, hipStream_t s) {
+    if (!two) return 0;
+    if (int e = herr(hipEventRecord(sc->lane_join, sc->lane1_main))) return e;
+    if (int e = herr(hipStreamWaitEvent(s, sc->lane_join, 0))) return e;
+    const lgcn_sched* l1 = sc->lane1;
+    for (int i = 0; i < l1->n_aux; ++i) {
+        if (int e = herr(hipEventRecord(l1->join[i], l1->aux[i]))) return e;
+        if (int e = herr(hipStreamWaitEvent(s, l1->join[i], 0))) return e;
+    }
+    return 0;
+}
+
+int check_plan(const lgcn_hub_plan_t* p);
+
+int check_sides(const int32_t* rowptr, const int32_t* row_ids, int32_t n, int32_t split,
+                const lgcn_hub_plan_t* plans) {
+    if (!plans || !rowptr || (n > 0 && !row_ids) || split < 0 || split > n) return LGCN_EINVAL;
+    for (int i = 0; i < 4; ++i)
+        if (int e = check_plan(plans + i)) return e;
+    return 0;
+}
+
 int check_plan(const lgcn_hub_plan_t* p) {
     if (!p) return LGCN_EINVAL;
     if (p->n_items < 0 || (p->n_items > 0 && !p->items)) return LGCN_EINVAL;
@@ -804,16 +945,37 @@ int check_plan(const lgcn_hub_plan_t* p) {
 extern "C" {
 
 int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** out) {
-    if (!out || n_aux < 1 || n_aux > 3 || !aux_streams) return LGCN_EINVAL;
+    if (!out || n_aux < 1 || n_aux > 7 || !aux_streams) return LGCN_EINVAL;
+    for (int i = 0; i < n_aux; ++i)
+        if (!aux_streams[i]) return LGCN_EINVAL;
     lgcn_sched* sc = new (std::nothrow) lgcn_sched();
     if (!sc) return LGCN_EINVAL;
     memset(sc, 0, sizeof(*sc));
-    sc->n_aux = n_aux;
+    const int n0 = n_aux < 3 ? n_aux : 3;
+    sc->n_aux = n0;
     sc->chain = 1;
-    for (int i = 0; i < n_aux; ++i) sc->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[i]);
-    int e = herr(hipEventCreateWithFlags(&sc->fork, hipEventDisableTiming));
-    for (int i = 0; i < n_aux && !e; ++i)
-        e = herr(hipEventCreateWithFlags(&sc->join[i], hipEventDisableTiming));
+    for (int i = 0; i < n0; ++i) sc->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[i]);
+    auto mk = [](hipEvent_t* ev) { return herr(hipEventCreateWithFlags(ev, hipEventDisableTiming)); };
+    int e = mk(&sc->fork);
+    for (int i = 0; i < n0 && !e; ++i) e = mk(&sc->join[i]);
+    if (!e && n_aux >= 4) {
+        sc->lane1_main = reinterpret_cast<hipStream_t>(aux_streams[3]);
+        sc->lane1 = new (std::nothrow) lgcn_sched();
+        if (!sc->lane1) e = LGCN_EINVAL;
+        if (!e) {
+            memset(sc->lane1, 0, sizeof(*sc->lane1));
+            lgcn_sched* l1 = sc->lane1;
+            l1->n_aux = n_aux - 4;
+            l1->chain = 1;
+            for (int i = 0; i < l1->n_aux; ++i)
+                l1->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[4 + i]);
+            e = mk(&l1->fork);
+            for (int i = 0; i < l1->n_aux && !e; ++i) e = mk(&l1->join[i]);
+            if (!e) e = mk(&sc->lane_fork);
+            if (!e) e = mk(&sc->lane_join);
+            for (int i = 0; i < 2 && !e; ++i) e = mk(&sc->cross[i]);
+        }
+    }
     if (e) {
         lgcn_sched_destroy(sc);
         return e;
@@ -827,6 +989,10 @@ int lgcn_sched_destroy(lgcn_sched_t* sc) {
     if (sc->fork) (void)hipEventDestroy(sc->fork);
     for (int i = 0; i < 3; ++i)
         if (sc->join[i]) (void)hipEventDestroy(sc->join[i]);
+    hipEvent_t* own[] = {&sc->lane_fork, &sc->lane_join, &sc->cross[0], &sc->cross[1]};
+    for (hipEvent_t* ev : own)
+        if (*ev) (void)hipEventDestroy(*ev);
+    if (sc->lane1) lgcn_sched_destroy(sc->lane1);
     delete sc;
     return 0;
 }
@@ -838,9 +1004,11 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
         case LGCN_SCHED_SLOTS1:
             if (value < 0 || value > LGCN_EMU_MAX_WALK_SLOTS) return LGCN_EINVAL;
             sc->slots[knob - LGCN_SCHED_SLOTS0] = (int32_t)value;
+            if (sc->lane1) sc->lane1->slots[knob - LGCN_SCHED_SLOTS0] = (int32_t)value;
             return 0;
         case LGCN_SCHED_CHAIN:
             sc->chain = value != 0;
+            if (sc->lane1) sc->lane1->chain = value != 0;
             return 0;
         case LGCN_SCHED_TIMING_START:
             sc->t0 = reinterpret_cast<hipEvent_t>(value);
@@ -850,6 +1018,12 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
             return 0;
         case LGCN_SCHED_TRACE:
             sc->trace = reinterpret_cast<hipEvent_t*>(value);
+            return 0;
+        case LGCN_SCHED_TRACE_SIDES:
+            sc->trace_sides = reinterpret_cast<hipEvent_t*>(value);
+            return 0;
+        case LGCN_SCHED_TIMING_SIDES:
+            sc->timing_sides = reinterpret_cast<hipEvent_t*>(value);
             return 0;
         default:
             return LGCN_EINVAL;
@@ -909,6 +1083,94 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
         }
     }
     return 0;
+}
+
+int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
+                                 const int32_t* row_ids, int32_t n, int32_t split,
+                                 const lgcn_hub_plan_t* plans, lgcn_rows_t emb, int32_t d,
+                                 int32_t K, float* const* layer_bufs_host, float* out,
+                                 const lgcn_sched_t* sched, void* stream) {
+    if (int e = valid_geom(n, d)) return e;
+    if (K < 0 || K - 1 > LGCN_MAX_LAYERS || !out) return K < 0 || !out ? LGCN_EINVAL : LGCN_ETOOMANY;
+    if (K > 1 && !layer_bufs_host) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (K == 0) return scale_rows(emb, n, d, 1.0f, out, d, s);
+    if (int e = check_sides(rowptr, row_ids, n, split, plans)) return e;
+    Lane lanes[2];
+    const bool two = make_lanes(sched, s, lanes);
+    if (int e = fork_lanes(sched, two, s)) return e;  // lane 1 starts where `s` is (E0 ready)
+    for (int k = 1; k <= K; ++k) {
+        const lgcn_rows_t x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
+        lgcn_epilogue_t ep;
+        memset(&ep, 0, sizeof(ep));
+        float* y;
+        if (k < K) {
+            ep.mode = LGCN_EPI_STORE;
+            y = layer_bufs_host[k - 1];
+        } else {
+            ep.mode = LGCN_EPI_MEAN;
+            ep.n_prev = K;
+            ep.div = (float)(K + 1);
+            ep.prev0 = emb;
+            for (int i = 0; i + 1 < K; ++i) ep.prev_dense[i] = layer_bufs_host[i];
+            ep.ld_prev = d;
+            y = out;
+        }
+        // the item side first: its half-layer holds the longest walks (host submission order
+        // only; the two sides of one layer are independent)
+        for (int side = 1; side >= 0; --side) {
+            const Lane& L = lanes[(k + side) & 1];
+            // the mean of a side reads its layer K-1, computed on the other lane
+            if (two && k == K && K >= 2)
+                if (int e = herr(hipStreamWaitEvent(L.main, sched->cross[side], 0))) return e;
+            if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, x, 1.f,
+                                   nullptr, y, d, ep, sched, L))
+                return e;
+            if (two && k == K - 1)
+                if (int e = herr(hipEventRecord(sched->cross[side], L.main))) return e;
+        }
+    }
+    return join_lanes(sched, two, s);
+}
+
+int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
+                                  const int32_t* row_ids, int32_t n, int32_t split,
+                                  const lgcn_hub_plan_t* plans, lgcn_rows_t grad_out,
+                                  const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
+                                  float* grad_e0, const lgcn_sched_t* sched, void* stream) {
+    if (int e = valid_geom(n, d)) return e;
+    if (K < 0 || !grad_out.p0 || !grad_e0) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    if (K == 0) return scale_rows(grad_out, n, d, 1.0f, grad_e0, d, s);
+    if (K > 1 && !work_h) return LGCN_EINVAL;
+    if (int e = check_sides(rowptr, row_ids, n, split, plans)) return e;
+    Lane lanes[2];
+    const bool two = make_lanes(sched, s, lanes);
+    if (int e = fork_lanes(sched, two, s)) return e;
+    // as lgcn_propagate_backward; half-layer (k, side) reads layer k-1's other side, written on
+    // the same lane, and overwrites (alternate buffers) layer k-2's same side, which only the
+    // same lane's half-layer (k-1, other side) read
+    const float div = (float)(K + 1);
+    lgcn_epilogue_t ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.mode = LGCN_EPI_ADD;
+    ep.addend = grad_out;
+    ep.addend_nz = grad_nz;
+    ep.div = div;
+    lgcn_rows_t h = grad_out;
+    float xdiv = div;
+    const uint32_t* x_nz = grad_nz;
+    for (int k = 1; k <= K; ++k) {
+        float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
+        for (int side = 1; side >= 0; --side)
+            if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, h, xdiv, x_nz,
+                                   y, d, ep, sched, lanes[(k + side) & 1]))
+                return e;
+        h = dense_rows(y, n, d);
+        xdiv = 1.f;
+        x_nz = nullptr;
+    }
+    return join_lanes(sched, two, s);
 }
 
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,

@@ -27,10 +27,11 @@ TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3,
 TUNE_EMU_RESOLVE = 5
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
+SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
-ABI_VERSION = 8
+ABI_VERSION = 9
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -136,8 +137,10 @@ ABI = [
     ("lgcn_coo_sort_perm", ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P,
                                           ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_csr_check_symmetric", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P]),
-    ("lgcn_csr_order_by_degree", ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P,
-                                                _P, _P, ctypes.POINTER(ctypes.c_size_t), _P]),
+    ("lgcn_csr_order_by_degree", ctypes.c_int, [_P, _P, _I32, _I64, _I32, _I32, _P, _P, _P, _P, _P,
+                                                _P, _P, _P, _P, ctypes.POINTER(ctypes.c_size_t),
+                                                _P]),
+    ("lgcn_csr_check_bipartite", ctypes.c_int, [_P, _P, _P, _I32, _I64, _I32, _I32, _P, _P]),
     ("lgcn_csr_relabel_cols", ctypes.c_int, [_P, _I64, _P, _P, _P]),
     ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),  # (sorted keys, ...)
     ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
@@ -172,6 +175,10 @@ ABI = [
                                               _I32, _P, _P, _P, _P, _P]),
     ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _P,
                                                _I32, _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_forward_sides", ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.POINTER(PlanT),
+                                                    RowsT, _I32, _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_backward_sides", ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.POINTER(PlanT),
+                                                     RowsT, _P, _I32, _I32, _P, _P, _P, _P]),
 ]
 
 
@@ -353,12 +360,14 @@ class HubPlan:
         r0, r1 = int((nb > b0).sum()), int((nb > b1).sum())
         return [r0, r1], [int(cum[r0]), int(cum[r1])]
 
-    def scratch(self, d, device, n_blocks=None):
+    def scratch(self, d, device, n_blocks=None, scratch_set=0):
         """(partials, emu_rel, emu_meta, emu_stage) for width d, covering the first n_blocks
-        emulated blocks (the walked ones; default all), allocated once per width and grown on
-        demand (the layers of one operator run in stream order). release_scratch() drops it."""
+        emulated blocks (the walked ones; default all), allocated once per width and set and
+        grown on demand (the layers of one operator run in stream order; the bipartite lanes run
+        a side's consecutive layers concurrently, on sets 0 and 1). release_scratch() drops it."""
         n_blocks = self.n_emu_blocks if n_blocks is None else n_blocks
-        have = self._scratch.get(d)
+        key = (d, scratch_set)
+        have = self._scratch.get(key)
         if have is None or have[4] < n_blocks:
             f32 = dict(dtype=torch.float32, device=device)
             part = have[0] if have is not None else (
@@ -370,28 +379,28 @@ class HubPlan:
                                    device=device)
                 if emu_stage_enabled():
                     stage = torch.empty(n_blocks * (d + 1) * LGCN_EMU_BLOCK, **f32)
-            self._scratch[d] = (part, rel, meta, stage, n_blocks)
-        return self._scratch[d][:4]
+            self._scratch[key] = (part, rel, meta, stage, n_blocks)
+        return self._scratch[key][:4]
 
     def release_scratch(self, d=None):
         """Drop the cached scratch of width d (all widths: None); torch.cuda.empty_cache() can
         then return it."""
-        if d is None:
-            self._scratch.clear()
-        else:
-            self._scratch.pop(d, None)
+        for key in list(self._scratch):
+            if d is None or key[0] == d:
+                del self._scratch[key]
 
-    def struct(self, d, device, nnz=None, walk_all=False):
+    def struct(self, d, device, nnz=None, walk_all=False, scratch_set=0):
         """lgcn_hub_plan_t for width d. nnz: the operator's nonzeros (sets the chain/walk cut;
         None = every emulated row walked). walk_all: the chain rows are walked too (no chain
-        kernel for this d / alignment, or LGCN_CHAIN=0), so the scratch covers every block."""
+        kernel for this d / alignment, or LGCN_CHAIN=0), so the scratch covers every block.
+        scratch_set: which of the plan's scratch sets (0, 1) the layer uses."""
         if nnz is None or walk_all:
             rows = [self.n_emu_rows, self.n_emu_rows] if nnz is None else None
             blocks = [self.n_emu_blocks, self.n_emu_blocks] if nnz is None else None
         if nnz is not None:
             rows, blocks = self.walk_parts(nnz)
         need = self.n_emu_blocks if (walk_all or nnz is None) else blocks[1]
-        part, rel, meta, stage = self.scratch(d, device, need)
+        part, rel, meta, stage = self.scratch(d, device, need, scratch_set)
         p = PlanT()
         p.items, p.n_items = (self.items.data_ptr() if self.n_items else None), self.n_items
         p.rows, p.n_rows, p.n_pre = (self.rows.data_ptr() if self.n_entries else None), \
@@ -500,6 +509,10 @@ class Graph:
         self.row_ids = row_ids
         self.transpose = None
         self.symmetric = None
+        # bipartite slot order (order_by_degree with sides): rows of [sides[0], sides[1]) in
+        # slots [split, n), every other row in [0, split) — the two half-layers of a layer
+        self.sides = None
+        self.split = None
         self._plans = {}
         self._rowptr_host = None
         self._row_ids_host = None
@@ -531,6 +544,28 @@ class Graph:
                                          self.row_ids_host(), mode=mode, emu_min=emu_min)
         return self._plans[key]
 
+    def side_hubs(self, threshold, chunk=None, mode=None, emu_min=None):
+        """The hub plans (cached) of the two sides of a side-major graph: side 0 = slots
+        [0, split), side 1 = [split, n) — each over its slot range, row ids and edge offsets
+        absolute, as lgcn_propagate_*_sides takes them."""
+        if self.split is None:
+            raise LgcnError("side_hubs needs a side-ordered graph (graph_from_coo(adj, sides=...))")
+        mode = mode or hub_mode_from_env()
+        if mode not in HUB_MODES:
+            raise LgcnError(f"unknown hub mode {mode!r}")
+        emu_min = emu_min_degree_from_env() if emu_min is None else emu_min
+        chunk = chunk or hub_chunk_for(self.nnz)
+        key = ("sides", threshold, mode) + \
+            ((chunk, DEFAULT_HUB_PRE_GROUP) if mode == "chunk" else (emu_min,))
+        if key not in self._plans:
+            rp, ids = self.rowptr_host(), self.row_ids_host()
+            sp = self.split
+            self._plans[key] = [
+                plan_hubs(rp[a:b + 1], threshold, chunk, self.device, ids[a:b], mode=mode,
+                          emu_min=emu_min)
+                for a, b in ((0, sp), (sp, self.n_rows))]
+        return self._plans[key]
+
     def degrees(self):
         """Degree of every row, indexed by row id."""
         deg = np.diff(self.rowptr_host().astype(np.int64))
@@ -548,11 +583,13 @@ def slot_key_enabled(g):
     return g.n_rows == g.n_cols and os.environ.get("LGCN_SLOT_KEY", "1") != "0"
 
 
-def order_by_degree(lib, g, stream):
+def order_by_degree(lib, g, stream, sides=None):
     """The same operator with its rows stored in degree-descending slots (lgcn_csr_order_by_degree):
     lane groups of a wave then stream rows of equal length; ties grouped by neighbour key
-    (slot_key_enabled). Bitwise-neutral."""
+    (slot_key_enabled). sides=(lo, hi): rows of [lo, hi) after all others (each side
+    degree-descending), the bipartite schedule's slot order. Bitwise-neutral."""
     n, nnz, dev = g.n_rows, g.nnz, g.device
+    lo, hi = sides if sides is not None else (0, 0)
     i32 = dict(dtype=torch.int32, device=dev)
     deg_tmp, deg_sorted, iota = (torch.empty(max(n, 1), **i32) for _ in range(3))
     row_ids = torch.empty(max(n, 1), **i32)
@@ -562,7 +599,8 @@ def order_by_degree(lib, g, stream):
         if slot_key_enabled(g) else (None, None)
     key_tmp, key_sorted = keys
     nbytes = ctypes.c_size_t(0)
-    args = (_ptr(g.rowptr), _ptr(g.edges), n, nnz, _ptr(deg_tmp), _ptr(deg_sorted), _ptr(iota),
+    args = (_ptr(g.rowptr), _ptr(g.edges), n, nnz, lo, hi, _ptr(deg_tmp), _ptr(deg_sorted),
+            _ptr(iota),
             _ptr(row_ids), _ptr(rowptr), _ptr(edges),
             _ptr(key_tmp) if key_tmp is not None else None,
             _ptr(key_sorted) if key_sorted is not None else None)
@@ -574,7 +612,27 @@ def order_by_degree(lib, g, stream):
     del deg_tmp, deg_sorted, iota, temp, key_tmp, key_sorted
     o = Graph(n, g.n_cols, rowptr, edges, nnz, dev, row_ids=row_ids[:n])
     o.symmetric = g.symmetric
+    if lo < hi:
+        o.sides, o.split = (lo, hi), n - (hi - lo)
     return o
+
+
+def sides_min_nnz():
+    """Graphs from this many nonzeros run the bipartite schedule when the caller names the sides
+    (LGCN_SIDES_MIN_NNZ, default 2^20; LGCN_SIDES=0 turns it off): below it a layer is a few
+    launches and splitting them only adds launch latency."""
+    if os.environ.get("LGCN_SIDES", "1") == "0":
+        return None
+    return int(os.environ.get("LGCN_SIDES_MIN_NNZ", str(1 << 20)))
+
+
+def is_bipartite(lib, g, sides, stream):
+    """lgcn_csr_check_bipartite: every edge joins a row inside [lo, hi) to one outside."""
+    bad = torch.zeros(1, dtype=torch.int32, device=g.device)
+    _check(lib.lgcn_csr_check_bipartite(_ptr(g.rowptr), _ptr(g.edges), _ptr(g.row_ids), g.n_rows,
+                                        g.nnz, sides[0], sides[1], _ptr(bad), stream),
+           "lgcn_csr_check_bipartite")
+    return int(bad.item()) == 0
 
 
 def _coo_to_csr(lib, key, other, vals, nnz, n_keys, device, stream, sort):
@@ -623,9 +681,10 @@ def relabel_slots(g):
 
 
 def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, cols_sorted,
-                  order=None):
+                  order=None, sides=None):
     """Attach the backward operator: Â itself if bitwise symmetric, else a stably sorted Âᵀ;
-    then store both in the processing order (row_order())."""
+    then store both in the processing order (row_order()) — side-major when `sides` = (lo, hi)
+    is given, Â is bipartite across it and large enough (sides_min_nnz)."""
     g = Graph(n, n, rowptr, edges, nnz, device)
     symmetric = False
     if cols_sorted:
@@ -641,8 +700,12 @@ def _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream, 
         t = Graph(n, n, t_rowptr, t_edges, nnz, device)
         t.symmetric = False
     if row_order(order) == "degree":
-        g = order_by_degree(lib, g, stream)
-        t = order_by_degree(lib, t, stream) if t is not None else None
+        mn = sides_min_nnz()
+        if sides is not None and (mn is None or nnz < mn or sides[0] >= sides[1] or
+                                  not is_bipartite(lib, g, sides, stream)):
+            sides = None  # (Âᵀ is bipartite across the same cut when Â is)
+        g = order_by_degree(lib, g, stream, sides)
+        t = order_by_degree(lib, t, stream, sides) if t is not None else None
     if t is None:
         g.transpose = g
     else:
@@ -656,20 +719,23 @@ def _cache_key(adj):
             tuple(adj.shape), str(adj.device))
 
 
-def attach_graph(adj, g):
+def attach_graph(adj, g, sides=None):
     """Cache a prepared Graph on the adjacency tensor it was built from."""
     try:
-        adj._lgcn_graph = (_cache_key(adj), g)
+        adj._lgcn_graph = (_cache_key(adj) + (tuple(sides) if sides is not None else None,), g)
     except (AttributeError, RuntimeError):
         pass
     return adj
 
 
-def graph_from_coo(adj):
+def graph_from_coo(adj, sides=None):
     """Convert the caller-owned sparse COO Â (main.py:334-336) into the engine's CSR, once.
 
     The plan is cached on the tensor object and re-validated by storage pointers and version
     counters, so the per-batch call `model(norm_adj_tensor)` (main.py:495) costs nothing extra.
+    sides: optional (lo, hi) — the item rows [U, U+I) of main.py:283-287: when Â is bipartite
+    across them (users and brands link only to items) the graph is stored side-major and the
+    propagation runs the bipartite two-lane schedule (lgcn_propagate_*_sides).
     """
     if not adj.is_sparse or adj.layout != torch.sparse_coo:
         raise LgcnError("adj_mat must be a torch.sparse_coo_tensor")
@@ -679,7 +745,7 @@ def graph_from_coo(adj):
         raise LgcnError(f"adj_mat must be float32, got {adj.dtype}")
     idx = adj._indices()
     vals = adj._values()
-    key = _cache_key(adj)
+    key = _cache_key(adj) + (tuple(sides) if sides is not None else None,)
     cached = getattr(adj, "_lgcn_graph", None)
     if cached is not None and cached[0] == key:
         return cached[1]
@@ -703,7 +769,8 @@ def graph_from_coo(adj):
         rowptr, edges = _coo_to_csr(lib, rows, cols, vals, nnz, n, device, stream,
                                     sort=bool(f & COO_ROWS_UNSORTED))
         g = _finish_graph(lib, rows, cols, vals, rowptr, edges, n, nnz, device, stream,
-                          cols_sorted=not (f & (COO_ROWS_UNSORTED | COO_COLS_UNSORTED)))
+                          cols_sorted=not (f & (COO_ROWS_UNSORTED | COO_COLS_UNSORTED)),
+                          sides=tuple(sides) if sides is not None else None)
     try:
         adj._lgcn_graph = (key, g)
     except (AttributeError, RuntimeError):
@@ -747,26 +814,37 @@ _scheds = {}
 
 def _side_stream(device, i=0):
     """Per-device side streams the emulated and chain rows run on beside the layer kernel
-    (lgcn_sched). Stream 0 carries the longest rows (the layer's critical path): it is created
-    at high priority (LGCN_EMU_PRIORITY=0: normal) so its waves are dispatched first."""
-    key = (str(device), i)
+    (lgcn_sched). Streams 0 and 4 carry the longest rows of lane 0 / lane 1 (a layer's critical
+    path): created at high priority (LGCN_EMU_PRIORITY=0: normal) so their waves are dispatched
+    first; stream 3 is lane 1's main stream."""
     sc = _scheds.setdefault(("streams", str(device)), {})
     if i not in sc:
-        hi = i < int(os.environ.get("LGCN_EMU_PRIORITY", "1"))  # streams 0..n-1 high priority
+        hi = i in (0, 4) and os.environ.get("LGCN_EMU_PRIORITY", "1") != "0"
         sc[i] = torch.cuda.Stream(device, priority=-1 if hi else 0)
     return sc[i]
 
 
+def hw_queues():
+    """Hardware queues HIP gives this process (GPU_MAX_HW_QUEUES, HIP's default 4)."""
+    try:
+        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        return 4
+
+
 def n_aux_streams():
-    """Auxiliary streams of the exact layer (LGCN_AUX_STREAMS, 1..3, default 3): with the
-    caller's stream 4 hardware queues (GPU_MAX_HW_QUEUES=4); at N > 1 RCCL's stream competes
-    for them, and the N > 1 path asks for 2."""
-    return max(1, min(3, int(os.environ.get("LGCN_AUX_STREAMS", "3"))))
+    """Auxiliary streams of the exact layers (LGCN_AUX_STREAMS, 1..7): 3 (parts 0 and 1 and the
+    chain rows beside the caller's stream) with HIP's 4 hardware queues; 7 (a second lane of
+    half-layers: its main stream + its own 3, lgcn_sched_create) when GPU_MAX_HW_QUEUES >= 8
+    gives every stream a queue. At N > 1 RCCL's stream competes for them (dist asks for fewer)."""
+    v = os.environ.get("LGCN_AUX_STREAMS", "")
+    n = int(v) if v else (7 if hw_queues() >= 8 else 3)
+    return max(1, min(7, n))
 
 
 class Sched:
     """lgcn_sched_t over this device's side streams (created once per device and stream count;
-    the C library owns the fork/join events)."""
+    the C library owns the fork/join events). n_aux >= 4: two lanes (lgcn_propagate_*_sides)."""
 
     def __init__(self, device, n_aux):
         lib = load_library()
@@ -793,12 +871,12 @@ class Sched:
             pass
 
 
-def sched_for(device):
+def sched_for(device, n_aux=None):
     """The device's Sched (None with LGCN_EMU_OVERLAP=0: every part in order on the caller's
-    stream)."""
+    stream). n_aux: default n_aux_streams()."""
     if not emu_overlap_enabled():
         return None
-    key = (str(device), n_aux_streams(), emu_slots_key(), chain_enabled())
+    key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled())
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
     return _scheds[key]
@@ -887,13 +965,79 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     return y
 
 
+def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned):
+    """The 4 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * side + set]."""
+    lib = load_library()
+    hps = graph.side_hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
+    chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and xs_aligned
+    arr = (PlanT * 4)()
+    for side in (0, 1):
+        for j in (0, 1):
+            arr[2 * side + j] = hps[side].struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
+                                                 scratch_set=j)
+    return arr, hps
+
+
+class _SideEvents:
+    """Timing / trace events of the sided entry points (SCHED_TIMING_SIDES / SCHED_TRACE_SIDES),
+    set on the schedule for one call and cleared after it."""
+
+    def __init__(self, sc, K, timing, trace):
+        self.sc = sc
+        self.timing = self.trace = None
+        self._arrs = []
+        if sc is None:
+            return
+        if timing:
+            self.timing = [torch.cuda.Event(enable_timing=True) for _ in range(4 * K)]
+            self._set(SCHED_TIMING_SIDES, self.timing)
+        if trace:
+            self.trace = [torch.cuda.Event(enable_timing=True) for _ in range(16 * K)]
+            self._set(SCHED_TRACE_SIDES, self.trace)
+
+    def _set(self, knob, evs):
+        for ev in evs:  # materialise the hipEvent_t handles
+            ev.record()
+        arr = (ctypes.c_void_p * len(evs))(*[ev.cuda_event for ev in evs])
+        self._arrs.append(arr)
+        self.sc.set(knob, ctypes.addressof(arr))
+
+    def clear(self):
+        if self.sc is not None:
+            self.sc.set(SCHED_TIMING_SIDES, 0)
+            self.sc.set(SCHED_TRACE_SIDES, 0)
+
+
+side_trace = None   # a list: the sided entry points append {(k, side): [(phase, event)]} per call
+side_timing = None  # a list: ... append {(k, side): (start, end)} around each half-layer kernel
+
+
+def use_sides(graph, layer_events=None, kernel_events=None):
+    """The bipartite schedule runs when the graph is side-ordered (graph_from_coo with sides)
+    and no per-layer events are asked for (a layer has no single boundary in it)."""
+    return graph.split is not None and layer_events is None and kernel_events is None
+
+
+def _collect_sides(ev, K):
+    if ev.timing is not None and side_timing is not None:
+        side_timing.append({(k, s): (ev.timing[((k - 1) * 2 + s) * 2],
+                                     ev.timing[((k - 1) * 2 + s) * 2 + 1])
+                            for k in range(1, K + 1) for s in (0, 1)})
+    if ev.trace is not None and side_trace is not None:
+        side_trace.append({(k, s): list(zip(TRACE_PHASES, ev.trace[((k - 1) * 2 + s) * 8:
+                                                                    ((k - 1) * 2 + s + 1) * 8]))
+                           for k in range(1, K + 1) for s in (0, 1)})
+
+
 def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
                       return_layers=False, hub_mode=None, emu_min=None, kernel_events=None):
     """final = mean(E0, Â E0, ..., Â^K E0) with E0 = cat(segments) (never materialised).
 
     layer_events: optional list of (start, end) torch.cuda.Event pairs recorded on the current
     stream around each whole layer (every stream of it joined); kernel_events: the same around
-    each layer's layer-kernel launch alone (spmm_layer) — bench.py's live timing.
+    each layer's layer-kernel launch alone (spmm_layer) — bench.py's live timing. A side-ordered
+    graph runs the bipartite two-lane schedule (lgcn_propagate_forward_sides) unless per-layer
+    events are asked for.
     """
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
@@ -913,8 +1057,23 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
         if K == 0:
             _check(lib.lgcn_scale_rows(e0, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
             return (out, []) if return_layers else out
-        hp = graph.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         layers = [torch.empty((n, d), dtype=torch.float32, device=dev) for _ in range(K - 1)]
+        if use_sides(graph, layer_events, kernel_events):
+            plans, _ = _side_plans(graph, d, hub_threshold, hub_mode, emu_min,
+                                   _aligned16(segments))
+            sc = sched_for(dev)
+            ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
+            bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
+            try:
+                _check(lib.lgcn_propagate_forward_sides(
+                    _ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), n, graph.split,
+                    plans, e0, d, K, bufs, _ptr(out), sc.handle if sc is not None else None,
+                    stream), "lgcn_propagate_forward_sides")
+            finally:
+                ev.clear()
+            _collect_sides(ev, K)
+            return (out, layers) if return_layers else out
+        hp = graph.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         for k in range(1, K + 1):
             xs = segments if k == 1 else [layers[k - 2]]
             if k < K:
@@ -986,7 +1145,6 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         if K == 0:
             _check(lib.lgcn_scale_rows(g, n, d, 1.0, _ptr(out), d, stream), "lgcn_scale_rows")
             return out
-        hp = gt.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         mode = sparse or _sparse_grad_mode()
         nz = None
         if mode in ("auto", "on") and n > 0:
@@ -994,6 +1152,21 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
             # G (0.7 ms at C3) and a dense G runs the masked kernels at the dense rate
             nz, _ = rows_nonzero(segs, d, dev)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
+        if use_sides(gt):
+            plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs))
+            sc = sched_for(dev)
+            ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
+            try:
+                _check(lib.lgcn_propagate_backward_sides(
+                    _ptr(gt.rowptr), _ptr(gt.edges), _ptr(gt.row_ids), n, gt.split, plans, g,
+                    _ptr(nz), d, K, _ptr(work), _ptr(out),
+                    sc.handle if sc is not None else None, stream),
+                    "lgcn_propagate_backward_sides")
+            finally:
+                ev.clear()
+            _collect_sides(ev, K)
+            return out
+        hp = gt.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         ep = _epilogue(LGCN_EPI_ADD, addend=g, div=float(K + 1))
         ep.addend_nz = None if nz is None else nz.data_ptr()
         h = segs
@@ -1056,10 +1229,20 @@ class PropagateFunction(torch.autograd.Function):
         return (None, None, None) + tuple(torch.split(g0, ctx.sizes, 0))
 
 
+def segment_sides(segments):
+    """(lo, hi) of the second segment's rows — the items of cat(user, item, brand)
+    (main.py:283-287) — or None for fewer than two segments."""
+    if len(segments) < 2:
+        return None
+    lo = int(segments[0].shape[0])
+    return (lo, lo + int(segments[1].shape[0]))
+
+
 def propagate_blocks(adj, segments, K, hub_threshold=None):
     """Autograd-aware engine entry used by models.LightGCN / LightGCN_Fusion on a HIP device:
-    returns the final embeddings as one block per input segment (user, item, brand)."""
-    graph = graph_from_coo(adj)
+    returns the final embeddings as one block per input segment (user, item, brand). The item
+    rows are offered as the bipartite sides (graph_from_coo)."""
+    graph = graph_from_coo(adj, sides=segment_sides(segments))
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
     return PropagateFunction.apply(graph, K, hub_threshold, *segments)

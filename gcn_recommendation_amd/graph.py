@@ -113,9 +113,11 @@ def build_norm_adj_device(train_user, train_item, U, I, B, ib_item=None, ib_bran
                       "lgcn_adj_finish")
         idx, vals = idx[:, :nnz], vals[:nnz]
         adj = torch.sparse_coo_tensor(idx, vals, (n, n))
+        # users and brands link only to items (main.py:295-311): the item rows are one side
+        sides = (U, U + I)
         g = engine._finish_graph(lib, adj._indices()[0], adj._indices()[1], adj._values(), rowptr,
-                                 edges, n, nnz, dev, st, cols_sorted=True)
-    return engine.attach_graph(adj, g)
+                                 edges, n, nnz, dev, st, cols_sorted=True, sides=sides)
+    return engine.attach_graph(adj, g, sides)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 8
+#define LGCN_ABI_VERSION 9
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -236,13 +236,27 @@ int lgcn_csr_check_symmetric(const int32_t* rowptr, const lgcn_edge_t* edges, in
  * square operators only: columns index rows), rows of equal degree are grouped by their least
  * popular neighbour (highest degree rank) — rows gathered by the same row then sit in
  * consecutive slots, which a narrow (featsplit) shard turns into shared 128-B lines.
+ * Sides: with side_lo < side_hi the rows in [side_lo, side_hi) (main.py:283-287: the items)
+ * take the last n_rows - (side_hi - side_lo) .. n_rows - 1 slots, every other row the first
+ * ones, each side degree-descending — the slot order the bipartite schedule
+ * (lgcn_propagate_forward_sides) cuts into its two half-layers. side_lo == side_hi: one order.
  * Scratch deg_tmp / deg_sorted / iota_tmp: n_rows int32 each. Two-call protocol for temp
  * (temp == NULL: only *temp_bytes_host is written; pass the same key pointers both times). */
 int lgcn_csr_order_by_degree(const int32_t* rowptr, const lgcn_edge_t* edges, int32_t n_rows,
-                             int64_t nnz, int32_t* deg_tmp, int32_t* deg_sorted, int32_t* iota_tmp,
+                             int64_t nnz, int32_t side_lo, int32_t side_hi, int32_t* deg_tmp,
+                             int32_t* deg_sorted, int32_t* iota_tmp,
                              int32_t* row_ids, int32_t* rowptr_out, lgcn_edge_t* edges_out,
                              uint64_t* key_tmp, uint64_t* key_sorted,
                              void* temp, size_t* temp_bytes_host, void* stream);
+
+/* Bipartite test for the schedule of lgcn_propagate_*_sides: *bad (device int32, zeroed by the
+ * caller) becomes nonzero if some edge joins two rows on the same side of [side_lo, side_hi)
+ * (a row inside the range linked to another inside, or outside to outside). row_ids: the slot
+ * order (NULL = rows stored in id order). The reference graph passes: users and brands link only
+ * to items (main.py:295-311). */
+int lgcn_csr_check_bipartite(const int32_t* rowptr, const lgcn_edge_t* edges,
+                             const int32_t* row_ids, int32_t n_rows, int64_t nnz,
+                             int32_t side_lo, int32_t side_hi, int32_t* bad, void* stream);
 
 /* Column relabelling: edges_out[j] = edges[j] with column c replaced by new_id[c]. With the
  * slot order of lgcn_csr_order_by_degree (new_id = its inverse) this stores P·Â·Pᵀ: an operator
@@ -339,13 +353,20 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                     void* stream);
 
 /* Concurrent schedule of the exact layers (lgcn_layer, lgcn_propagate_forward/backward): the
- * emulated and chain rows run on 1..3 auxiliary streams beside the layer kernel, forked from and
+ * emulated and chain rows run on auxiliary streams beside the layer kernel, forked from and
  * joined back into the caller's stream by events (graph-capture safe). Part 0 (the longest rows,
  * whose walk is a layer's critical path) goes to aux_streams[0] — create it with a high
  * priority — part 1 to [1], the chain rows to [2]; with fewer streams the later parts share the
- * last one (a budget for GPU_MAX_HW_QUEUES with RCCL running). lgcn_sched_create allocates the
- * events (the only allocating call; once per stream set); NULL sched = everything in order on
- * the caller's stream. */
+ * last one (a budget for GPU_MAX_HW_QUEUES with RCCL running).
+ * Bipartite lanes (lgcn_propagate_*_sides): with n_aux = 4 + m (m = 0..3), aux_streams[3] is
+ * the main stream of the second lane of half-layers and [4..3+m] its part 0 / part 1 / chain
+ * streams ([4] high priority), so the two chains of half-layers run side by side; with n_aux <= 3
+ * both lanes share the caller's stream and [0..2]. Every stream, the caller's included, wants a
+ * hardware queue of its own: 8 streams need GPU_MAX_HW_QUEUES >= 8 in the environment before
+ * the process first touches the GPU (HIP's default is 4; with fewer queues streams share them
+ * and the lanes partly serialise — same results).
+ * lgcn_sched_create allocates the events (the only allocating call; once per stream set); NULL
+ * sched = everything in order on the caller's stream. */
 typedef struct lgcn_sched lgcn_sched_t;
 int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** out);
 int lgcn_sched_destroy(lgcn_sched_t* sched);
@@ -357,6 +378,12 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
 #define LGCN_SCHED_TRACE         6  /* hipEvent_t[8] (or 0): per-layer phase events — fork, part 0
                                        and part 1 block passes done, layer kernel done, chains
                                        done, part 0 and part 1 walks done, joined */
+#define LGCN_SCHED_TRACE_SIDES   7  /* hipEvent_t[16 * K] (or 0): the same 8 phases of every
+                                       half-layer of lgcn_propagate_*_sides, half-layer (k, side)
+                                       at [((k - 1) * 2 + side) * 8] */
+#define LGCN_SCHED_TIMING_SIDES  8  /* hipEvent_t[4 * K] (or 0): recorded on its lane's stream right
+                                       before / after the layer kernel of half-layer (k, side), at
+                                       [((k - 1) * 2 + side) * 2] and [... + 1] (timing) */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +
@@ -388,6 +415,31 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
                             lgcn_rows_t grad_out,
                             const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                             float* grad_e0, const lgcn_sched_t* sched, void* stream);
+
+/* Bipartite propagation: the rows of one side reference only rows of the other (users and
+ * brands vs items, lgcn_csr_check_bipartite), so layer k of one side needs only layer k-1 of the
+ * other. Every layer runs as two half-layers — slots [0, split) and [split, n) of a side-major
+ * slot order (lgcn_csr_order_by_degree with side_lo < side_hi; split = its first slot of the
+ * range side) — on two lanes: half-layer (k, side) on lane (k + side) % 2, each lane a chain of
+ * half-layers that alternate sides. The longest rows' walks of one layer then overlap those of
+ * the next instead of queueing behind them. Same arguments and results (bitwise) as
+ * lgcn_propagate_forward / _backward, except:
+ *  - plans: 4 hub plans, plans[2 * side + j]: side's plan (built over its slot range, row ids
+ *    absolute) with two scratch sets j = 0, 1 (the half-layers of one side on consecutive layers
+ *    run on different lanes, concurrently with each other);
+ *  - row_ids is required; no per-layer timing events (LGCN_SCHED_TRACE_SIDES traces phases);
+ *  - forward: the final (mean) half-layer of a side also waits for that side's layer K-1 on the
+ *    other lane (the mean reads it). */
+int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
+                                 const int32_t* row_ids, int32_t n, int32_t split,
+                                 const lgcn_hub_plan_t* plans, lgcn_rows_t emb, int32_t d,
+                                 int32_t K, float* const* layer_bufs_host, float* out,
+                                 const lgcn_sched_t* sched, void* stream);
+int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
+                                  const int32_t* row_ids, int32_t n, int32_t split,
+                                  const lgcn_hub_plan_t* plans, lgcn_rows_t grad_out,
+                                  const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
+                                  float* grad_e0, const lgcn_sched_t* sched, void* stream);
 
 /* ---- training batch loss (main.py:366-402) -------------------------------------------------- */
 /* Fused BPR + L2 loss of one batch of B gathered rows (u, p, n = final user / positive /

@@ -52,7 +52,8 @@ class LightGCN(nn.Module):
             if self.debug and self.n_layers > 0:  # lightgcn.py:44-51 prints once per layer
                 with torch.no_grad():
                     _, layers = engine.propagate_forward(
-                        engine.graph_from_coo(adj_mat), [s.detach() for s in segments],
+                        engine.graph_from_coo(adj_mat, engine.segment_sides(segments)),
+                        [s.detach() for s in segments],
                         self.n_layers, return_layers=True)
                     off = self.num_users + self.num_items
                     for i, e in enumerate(layers + [None]):
@@ -73,7 +74,7 @@ class LightGCN(nn.Module):
         return torch.split(final, [self.num_users, self.num_items, self.num_brands])
 
     def _last_layer(self, adj_mat, layers, segments):
-        g = engine.graph_from_coo(adj_mat)
+        g = engine.graph_from_coo(adj_mat, engine.segment_sides(segments))
         x = layers[-1] if layers else torch.cat([s.detach() for s in segments], 0)
         y = torch.empty_like(x)
         return engine.spmm_layer(g, [x], y, x.shape[1], engine._epilogue(engine.LGCN_EPI_STORE),

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 8
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 9
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -83,11 +83,13 @@ def test_argument_validation_without_gpu(lib):
     plan.emu_part_rows[0], plan.emu_part_rows[1] = 1, 0  # parts out of order
     assert lib.lgcn_layer(None, None, None, 0, ctypes.byref(plan), rows, 1.0, None, None, 64, 64,
                           ctypes.byref(ep), None, None) == -1
-    # the schedule: 1..3 auxiliary streams; its knobs validated before any HIP call
+    # the schedule: 1..7 auxiliary streams (4..7: a second lane); its knobs validated before
+    # any HIP call
     h = ctypes.c_void_p()
     assert lib.lgcn_sched_create(None, 2, ctypes.byref(h)) == -1
-    arr = (ctypes.c_void_p * 4)()
-    assert lib.lgcn_sched_create(arr, 4, ctypes.byref(h)) == -1
+    arr = (ctypes.c_void_p * 8)()
+    assert lib.lgcn_sched_create(arr, 4, ctypes.byref(h)) == -1   # null streams
+    assert lib.lgcn_sched_create(arr, 8, ctypes.byref(h)) == -1
     assert lib.lgcn_sched_create(arr, 0, ctypes.byref(h)) == -1
     assert lib.lgcn_sched_set(None, engine.SCHED_SLOTS0, 4) == -1
     assert lib.lgcn_sched_destroy(None) == 0
@@ -107,15 +109,28 @@ def test_argument_validation_without_gpu(lib):
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
                                   ctypes.byref(nbytes), None) == -1
-    assert lib.lgcn_csr_order_by_degree(None, None, -1, 0, None, None, None, None, None, None,
-                                        None, None, None, ctypes.byref(nbytes), None) == -1
-    assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, None, None, None, None, None, None,
-                                        None, None, ctypes.c_void_p(1), ctypes.byref(nbytes),
+    assert lib.lgcn_csr_order_by_degree(None, None, -1, 0, 0, 0, None, None, None, None, None,
+                                        None, None, None, None, ctypes.byref(nbytes), None) == -1
+    assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, 0, 0, None, None, None, None, None,
+                                        None, None, None, ctypes.c_void_p(1), ctypes.byref(nbytes),
                                         None) == -1
     # the two key buffers come together or not at all
-    assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, None, None, None, None, None, None,
-                                        ctypes.c_void_p(8), None, None, ctypes.byref(nbytes),
+    assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, 0, 0, None, None, None, None, None,
+                                        None, ctypes.c_void_p(8), None, None, ctypes.byref(nbytes),
                                         None) == -1
+    # sides must lie inside [0, n_rows]
+    for lo, hi in ((-1, 3), (5, 4), (2, 11)):
+        assert lib.lgcn_csr_order_by_degree(None, None, 10, 0, lo, hi, None, None, None, None,
+                                            None, None, None, None, None, ctypes.byref(nbytes),
+                                            None) == -1
+    assert lib.lgcn_csr_check_bipartite(None, None, None, 10, 5, 3, 2, None, None) == -1
+    assert lib.lgcn_csr_check_bipartite(None, None, None, 10, 0, 2, 3, ctypes.c_void_p(4),
+                                        None) == 0   # no edges: nothing to check
+    # the sided entry points: four plans and the slot order are required
+    assert lib.lgcn_propagate_forward_sides(None, None, None, 5, 2, None, rows, 64, 2,
+                                            None, ctypes.c_void_p(8), None, None) == -1
+    assert lib.lgcn_propagate_backward_sides(None, None, None, 5, 2, None, rows, None, 64, 1,
+                                             None, ctypes.c_void_p(8), None, None) == -1
 
 
 def test_struct_layout_matches_header():
