@@ -483,8 +483,9 @@ def test_plan_cache_reused_and_invalidated(gpu_device):
 
 @ORDERS
 def test_c2_scale_uniform_and_powerlaw(gpu_device, order):
-    """BASELINE configs[1] shapes (50k x 50k, 1M interactions, d=64, K=3): exact mode bitwise,
-    default mode within tolerance, forward and backward."""
+    """BASELINE configs[1] shapes (50k x 50k, 1M interactions, d=64, K=3): the default (exact)
+    plan bitwise forward and backward, on the one-operator and on the bipartite two-lane
+    schedule; the chunk plan within the north_star tolerance."""
     for gen in ("uniform", "powerlaw"):
         if gen == "uniform":
             u, i = graph.uniform_interactions(50_000, 50_000, 1_000_000, 1)
@@ -502,13 +503,25 @@ def test_c2_scale_uniform_and_powerlaw(gpu_device, order):
         e0 = np.random.default_rng(0).standard_normal((U + I, 64)).astype(np.float32) * 0.01
         x = [torch.from_numpy(e0).to(gpu_device)]
         want = oracle.forward(r, c, v, e0, 3)
-        exact = engine.propagate_forward(g, x, 3, hub_threshold=engine.INT32_MAX)
-        assert np.array_equal(exact.cpu().numpy(), want), gen
-        fast = engine.propagate_forward(g, x, 3).cpu().numpy()
-        assert_close_normwise(fast, want, what=gen)
+        seq = engine.propagate_forward(g, x, 3, hub_threshold=engine.INT32_MAX)
+        assert np.array_equal(seq.cpu().numpy(), want), gen
         G = np.random.default_rng(1).standard_normal((U + I, 64)).astype(np.float32)
-        gb = engine.propagate_backward(g, torch.from_numpy(G).to(gpu_device), 3).cpu().numpy()
-        assert_close_normwise(gb, oracle.backward(r, c, v, G, 3), what=gen + " bwd")
+        want_b = oracle.backward(r, c, v, G, 3)
+        gt = torch.from_numpy(G).to(gpu_device)
+        # the default plan (exact hub rows) on both schedules: bitwise
+        gs = engine.graph_from_coo(adj, sides=(U, U + I))
+        if order == "degree":
+            assert gs.split is not None  # Â of main.py:300-311 is bipartite across the items
+        for gg, sched in ((g, "one operator"), (gs, "two lanes")):
+            got = engine.propagate_forward(gg, x, 3).cpu().numpy()
+            assert np.array_equal(got, want), f"{gen} {sched} forward"
+            gb = engine.propagate_backward(gg, gt, 3).cpu().numpy()
+            assert np.array_equal(gb, want_b), f"{gen} {sched} backward"
+        # the chunk plan: deterministic, not the reference's rounding on long rows
+        fast = engine.propagate_forward(g, x, 3, hub_mode="chunk").cpu().numpy()
+        assert_close_normwise(fast, want, what=gen + " chunk")
+        gb = engine.propagate_backward(g, gt, 3, hub_mode="chunk").cpu().numpy()
+        assert_close_normwise(gb, want_b, what=gen + " chunk bwd")
 
 
 @ORDERS
