@@ -20,7 +20,9 @@
 #include "lgcn_kernels.h"
 
 #include <string.h>
+#include <algorithm>
 #include <new>
+#include <vector>
 
 namespace lgcn_detail {
 int g_rows_per_group = 0;
@@ -423,6 +425,81 @@ const char* lgcn_error_string(int code) {
     }
     if (code > 0) return hipGetErrorString((hipError_t)code);
     return "lgcn: unknown error";
+}
+
+int32_t lgcn_chain_max_default(int64_t nnz) {
+    // a chain row must stay short against a whole layer (C3: 56M nonzeros, ~3 ms per layer ->
+    // 55k edges; C2: 1.6M, ~0.07 ms -> the 2048 floor)
+    return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 1024, 2048), 65536);
+}
+
+int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,
+                    int32_t emu_min_degree, int32_t chain_max, int32_t part0_blocks,
+                    lgcn_emu_row_t* rows_host, lgcn_emu_block_t* blocks_host,
+                    lgcn_hub_plan_t* plan) {
+    if (!plan || n_rows < 0 || (n_rows > 0 && !rowptr_host) || emu_min_degree < 0)
+        return LGCN_EINVAL;
+    if ((rows_host == nullptr) != (blocks_host == nullptr)) return LGCN_EINVAL;
+    constexpr int64_t B = LGCN_EMU_BLOCK;
+    if (n_rows > 0 && (rowptr_host[0] < 0 || rowptr_host[n_rows] < rowptr_host[0]))
+        return LGCN_EINVAL;
+    if (chain_max <= 0)
+        chain_max = lgcn_chain_max_default(n_rows > 0 ? rowptr_host[n_rows] - rowptr_host[0] : 0);
+    if (part0_blocks <= 0) part0_blocks = 8192;
+    // the emulated rows, longest first; equal degrees keep their slot order
+    std::vector<int32_t> em;
+    for (int32_t s = 0; s < n_rows; ++s) {
+        const int64_t deg = (int64_t)rowptr_host[s + 1] - rowptr_host[s];
+        if (deg < 0) return LGCN_EINVAL;
+        if (deg > emu_min_degree) em.push_back(s);
+    }
+    std::stable_sort(em.begin(), em.end(), [&](int32_t a, int32_t b) {
+        return rowptr_host[a + 1] - rowptr_host[a] > rowptr_host[b + 1] - rowptr_host[b];
+    });
+    const int64_t b1 = (chain_max + B - 1) / B;                  // chain rows: <= b1 blocks
+    const int64_t b0 = std::max<int64_t>(part0_blocks, b1);      // part 0: > b0 blocks
+    int64_t nb_total = 0;
+    int32_t pr[2] = {0, 0}, pb[2] = {0, 0};
+    for (size_t i = 0; i < em.size(); ++i) {
+        const int32_t s = em[i];
+        const int64_t beg = rowptr_host[s], deg = (int64_t)rowptr_host[s + 1] - beg;
+        const int64_t nb = (deg + B - 1) / B;
+        if (nb_total + nb > INT32_MAX) return LGCN_EINVAL;
+        if (nb > b0) pr[0] = (int32_t)(i + 1), pb[0] = (int32_t)(nb_total + nb);
+        if (nb > b1) pr[1] = (int32_t)(i + 1), pb[1] = (int32_t)(nb_total + nb);
+        if (rows_host) {
+            rows_host[i].row = row_ids_host ? row_ids_host[s] : s;
+            rows_host[i].first_block = (int32_t)nb_total;
+            rows_host[i].n_blocks = (int32_t)nb;
+            rows_host[i].pad = 0;
+            for (int64_t k = 0; k < nb; ++k) {
+                lgcn_emu_block_t& bl = blocks_host[nb_total + k];
+                bl.row = (int32_t)i;
+                bl.beg = (int32_t)(beg + k * B);
+                bl.end = (int32_t)std::min(beg + (k + 1) * B, beg + deg);
+                bl.first = k == 0;
+            }
+        }
+        nb_total += nb;
+    }
+    plan->n_emu_rows = (int32_t)em.size();
+    plan->n_emu_blocks = (int32_t)nb_total;
+    plan->emu_part_rows[0] = pr[0];
+    plan->emu_part_rows[1] = pr[1];
+    plan->emu_part_blocks[0] = pb[0];
+    plan->emu_part_blocks[1] = pb[1];
+    plan->emu_scratch_blocks = pb[1];
+    return 0;
+}
+
+int lgcn_plan_scratch_bytes(const lgcn_hub_plan_t* plan, int32_t d, int32_t walk_all,
+                            size_t* bytes_host) {
+    if (!plan || !bytes_host || d < 1 || d > 2048) return LGCN_EINVAL;
+    const int64_t nb = walk_all ? plan->n_emu_blocks : plan->emu_part_blocks[1];
+    bytes_host[0] = (size_t)nb * d * LGCN_EMU_CANDS * 4;
+    bytes_host[1] = (size_t)nb * d * LGCN_EMU_META_BYTES;
+    bytes_host[2] = (size_t)nb * (d + 1) * LGCN_EMU_BLOCK * 4;
+    return 0;
 }
 
 int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host) {

@@ -31,7 +31,7 @@ SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
-ABI_VERSION = 9
+ABI_VERSION = 10
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -72,12 +72,13 @@ def emu_min_degree_from_env():
 def chain_max_degree(nnz):
     """Rows of the emulated-row list up to this degree run as sequential chains (lgcn_chain_rows,
     ~16 ns per edge), longer ones are block-emulated (block pass + walk): env LGCN_CHAIN_MAX, else
-    by graph size — a chain must stay short against the whole layer (C3: 56M nonzeros, ~3 ms per
-    layer -> 55k edges; C2: 1.6M, ~0.07 ms -> the 2048 floor)."""
+    by graph size (lgcn_chain_max_default: a chain must stay short against the whole layer)."""
     v = os.environ.get("LGCN_CHAIN_MAX", "")
     if v:
         return int(v)
-    return int(min(max(nnz // 1024, 2048), 65536))
+    return int(load_library().lgcn_chain_max_default(int(nnz)))
+
+
 # Edges per hub chunk: LGCN_HUB_CHUNK, else by graph size (hub_chunk_for). A chunk is one lane
 # group's sequential chain, so it must stay short against the whole layer: on the C2 graph
 # (1.6M nonzeros, 0.07-0.1 ms per layer) 128-edge chunks run the forward 0.318 -> 0.224 ms,
@@ -150,6 +151,9 @@ ABI = [
                                      _I32, _I32, ctypes.c_float, _P, _P, _P, _P]),
     ("lgcn_fusion_prelayer", ctypes.c_int, [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P,
                                             ctypes.c_float, _P, _I64, _P]),
+    ("lgcn_chain_max_default", ctypes.c_int32, [_I64]),
+    ("lgcn_plan_exact", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
+    ("lgcn_plan_scratch_bytes", ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(ctypes.c_size_t)]),
     ("lgcn_eval_splits", ctypes.c_int, [_I32, _I32, _I32]),
     ("lgcn_score_topk", ctypes.c_int, [_P, _I64, _P, _I32, _P, _I64, _I32, _I32, _P, _P, _I32,
                                        _I32, _P, _P, _P, _P, _P]),
@@ -419,26 +423,27 @@ class HubPlan:
         return p
 
 
-def plan_emulation(rowptr_host, slots, device, row_ids_host=None):
-    """Blocks of LGCN_EMU_BLOCK edges for the emulated rows, longest row first whatever the slot
-    order (the walks of the longest rows are a layer's critical path, and emu_parts cuts the rows
-    by length). Returns (blocks, rows) on the device and the host block counts per row."""
-    if slots.size == 0:
+def plan_emulation(rowptr_host, min_degree, device, row_ids_host=None):
+    """Every row of degree > min_degree as an emulated row, in blocks of LGCN_EMU_BLOCK edges,
+    longest row first whatever the slot order (the walks of the longest rows are a layer's
+    critical path; walk_parts cuts the rows by length): the C planner lgcn_plan_exact. Returns
+    (blocks, rows) on the device and the host block counts per row."""
+    lib = load_library()
+    rp = np.ascontiguousarray(rowptr_host, dtype=np.int32)
+    n = rp.size - 1
+    ids = None if row_ids_host is None else np.ascontiguousarray(row_ids_host, dtype=np.int32)
+    ids_p = None if ids is None else ids.ctypes.data
+    plan = PlanT()
+    _check(lib.lgcn_plan_exact(rp.ctypes.data, ids_p, n, int(min_degree), 0, 0, None, None,
+                               ctypes.byref(plan)), "lgcn_plan_exact(size)")
+    if plan.n_emu_rows == 0:
         return None, None, np.zeros(0, np.int64)
-    beg0 = rowptr_host[slots].astype(np.int64)
-    deg = rowptr_host[slots + 1].astype(np.int64) - beg0
-    order = np.argsort(-deg, kind="stable")
-    slots, beg0, deg = slots[order], beg0[order], deg[order]
-    nb = (deg + LGCN_EMU_BLOCK - 1) // LGCN_EMU_BLOCK
-    first = np.concatenate([[0], np.cumsum(nb)[:-1]])
-    ix = np.repeat(np.arange(slots.size), nb)
-    k = np.arange(int(nb.sum())) - np.repeat(first, nb)
-    beg = np.repeat(beg0, nb) + k * LGCN_EMU_BLOCK
-    end = np.minimum(beg + LGCN_EMU_BLOCK, np.repeat(beg0 + deg, nb))
-    blocks = np.stack([ix, beg, end, (k == 0).astype(np.int64)], 1).astype(np.int32)
-    out_row = slots if row_ids_host is None else row_ids_host[slots]
-    rows = np.stack([out_row, first, nb, np.zeros_like(nb)], 1).astype(np.int32)
-    return torch.from_numpy(blocks).to(device), torch.from_numpy(rows).to(device), nb
+    rows = np.empty((plan.n_emu_rows, 4), np.int32)
+    blocks = np.empty((plan.n_emu_blocks, 4), np.int32)
+    _check(lib.lgcn_plan_exact(rp.ctypes.data, ids_p, n, int(min_degree), 0, 0, rows.ctypes.data,
+                               blocks.ctypes.data, ctypes.byref(plan)), "lgcn_plan_exact")
+    return (torch.from_numpy(blocks).to(device), torch.from_numpy(rows).to(device),
+            rows[:, 2].astype(np.int64))
 
 
 def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_group=None,
@@ -465,7 +470,8 @@ def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_grou
         long_ = deg[hub] <= emu_min
         items = np.stack([out_row[long_], rowptr_host[hub[long_]], rowptr_host[hub[long_] + 1],
                           np.full(int(long_.sum()), -1)], 1).astype(np.int32)
-        eb, er, enb = plan_emulation(rowptr_host, hub[~long_], device, row_ids_host)
+        eb, er, enb = plan_emulation(rowptr_host, max(threshold, emu_min), device,
+                                     row_ids_host)
         return HubPlan(threshold, mode, None,
                        torch.from_numpy(items).to(device) if items.shape[0] else None,
                        emu_blocks=eb, emu_rows=er, emu_min=emu_min, emu_nb=enb)

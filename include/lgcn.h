@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 9
+#define LGCN_ABI_VERSION 10
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -162,6 +162,29 @@ typedef struct {
     int32_t emu_part_blocks[2];
     int32_t emu_scratch_blocks;
 } lgcn_hub_plan_t;
+
+/* Host planner of an exact hub plan (host memory only, no GPU call): from the host row pointers
+ * of the CSR as stored (slot order when row_ids_host != NULL: slot s holds row row_ids_host[s]),
+ * every row of degree > emu_min_degree becomes an emulated row — longest first, equal degrees in
+ * slot order — cut into LGCN_EMU_BLOCK-edge blocks: rows_host[n_emu_rows], blocks_host
+ * [n_emu_blocks] (copy both to the device for plan->emu_rows / emu_blocks). Part 0 = rows of
+ * more than max(part0_blocks, ceil(chain_max / LGCN_EMU_BLOCK)) blocks, part 1 = rows of more
+ * than ceil(chain_max / LGCN_EMU_BLOCK), the rest run as sequential chains (lgcn_chain_rows).
+ * Writes plan->n_emu_rows, n_emu_blocks, emu_part_rows, emu_part_blocks and emu_scratch_blocks
+ * (= emu_part_blocks[1]); nothing else. Two-call protocol: rows_host = blocks_host = NULL writes
+ * only the counts. chain_max <= 0: lgcn_chain_max_default(nnz); part0_blocks <= 0: 8192.
+ * emu_min_degree = the bundle threshold (128) for the default exact plan. Replaces, for a C
+ * host, the Python planner engine.plan_hubs (which calls it). */
+int32_t lgcn_chain_max_default(int64_t nnz);
+int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,
+                    int32_t emu_min_degree, int32_t chain_max, int32_t part0_blocks,
+                    lgcn_emu_row_t* rows_host, lgcn_emu_block_t* blocks_host,
+                    lgcn_hub_plan_t* plan);
+/* Scratch of a plan at width d: bytes_host[0..2] = emu_rel, emu_meta, emu_stage sizes covering
+ * the walked blocks (walk_all = 0: parts 0 and 1; 1: every emulated block, when chains cannot
+ * run — lgcn_chain_supported(d) false or X not 16-B aligned). */
+int lgcn_plan_scratch_bytes(const lgcn_hub_plan_t* plan, int32_t d, int32_t walk_all,
+                            size_t* bytes_host);
 
 /* Epilogue operands. MEAN: prev0 is a segmented block (E0), prev_dense[i] (i < n_prev-1) are the
  * dense layer buffers E1..E_{n_prev-1} with leading dimension ld_prev, div = K+1. ADD: addend

@@ -124,3 +124,45 @@ def test_rows_desc_from_addresses_global_rows():
                 addr = ptrs[2] + (i - ends[1]) * d * 4
             t, r = glob[start + i]
             assert addr == t.data_ptr() + r * d * 4, (start, i)
+
+
+def test_c_planner_parts_and_scratch():
+    """lgcn_plan_exact (the C host planner a C caller uses; engine.plan_hubs calls it): part cuts
+    by block count agree with walk_parts, scratch sizes follow lgcn.h, bad input is refused."""
+    import ctypes
+    lib = engine.load_library()
+    deg = np.array([5, 9000, 256 * 9000 + 3, 70_000, 129, 256 * 300, 256 * 8193 + 1, 128])
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    plan = engine.PlanT()
+    rc = lib.lgcn_plan_exact(rowptr.ctypes.data, None, deg.size, 128, 60_000, 8192, None, None,
+                             ctypes.byref(plan))
+    assert rc == 0
+    nb = sorted([-(-int(x) // 256) for x in deg if x > 128], reverse=True)
+    assert plan.n_emu_rows == len(nb) and plan.n_emu_blocks == sum(nb)
+    b1 = -(-60_000 // 256)
+    assert list(plan.emu_part_rows) == [sum(x > 8192 for x in nb), sum(x > b1 for x in nb)]
+    assert plan.emu_part_blocks[0] == sum(x for x in nb if x > 8192)
+    assert plan.emu_part_blocks[1] == plan.emu_scratch_blocks == sum(x for x in nb if x > b1)
+    rows = np.empty((plan.n_emu_rows, 4), np.int32)
+    blocks = np.empty((plan.n_emu_blocks, 4), np.int32)
+    assert lib.lgcn_plan_exact(rowptr.ctypes.data, None, deg.size, 128, 60_000, 8192,
+                               rows.ctypes.data, blocks.ctypes.data, ctypes.byref(plan)) == 0
+    assert list(rows[:, 2]) == nb
+    hp = engine.HubPlan(128, emu_nb=np.array(nb))
+    pr, pb = hp.walk_parts(60_000 * 1024)  # chain_max_degree(nnz) = 60_000 ... clamped to 65536
+    assert pr[0] == plan.emu_part_rows[0]
+    sizes = (ctypes.c_size_t * 3)()
+    assert lib.lgcn_plan_scratch_bytes(ctypes.byref(plan), 64, 0, sizes) == 0
+    nbw = plan.emu_part_blocks[1]
+    assert list(sizes) == [nbw * 64 * 16 * 4, nbw * 64 * 16, nbw * 65 * 256 * 4]
+    assert lib.lgcn_plan_scratch_bytes(ctypes.byref(plan), 64, 1, sizes) == 0
+    assert sizes[0] == plan.n_emu_blocks * 64 * 16 * 4
+    # refused: decreasing row pointers, rows without blocks
+    bad = np.array([0, 10, 5], np.int32)
+    assert lib.lgcn_plan_exact(bad.ctypes.data, None, 2, 0, 0, 0, None, None,
+                               ctypes.byref(plan)) == -1
+    assert lib.lgcn_plan_exact(rowptr.ctypes.data, None, deg.size, 128, 0, 0, rows.ctypes.data,
+                               None, ctypes.byref(plan)) == -1
+    assert lib.lgcn_chain_max_default(1_600_000) == 2048
+    assert lib.lgcn_chain_max_default(56_300_000) == 56_300_000 // 1024
+    assert lib.lgcn_chain_max_default(10 ** 10) == 65536
