@@ -844,9 +844,12 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
                const uint32_t* x_nz, float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep,
                const lgcn_sched* sc, hipStream_t s) {
     const int32_t ne = p.n_emu_rows;
-    const bool chains = ne > p.emu_part_rows[1] && chain_ok(x, d) && (!sc || sc->chain);
+    // row-sparse X (the backward's first layer on a BPR batch): every emulated row is a chain
+    // over its live edges (lgcn_live_rows) — no block pass, no walk
+    const bool live = x_nz && p.emu_live && ne > 0 && chain_ok(x, d) && (!sc || sc->chain);
+    const bool chains = !live && ne > p.emu_part_rows[1] && chain_ok(x, d) && (!sc || sc->chain);
     // walked rows read the block-pass scratch, which must cover their blocks
-    if ((chains ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
+    if (!live && (chains ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
         return LGCN_EINVAL;
     hipEvent_t* tr = sc ? sc->trace : nullptr;
     auto mark = [&](int k, hipStream_t st) -> int {
@@ -875,6 +878,26 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
         return lgcn_chain_rows(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, x, xdiv, y,
                                ldy, d, &ep, st);
     };
+    auto live_rows = [&](hipStream_t st) -> int {
+        return lgcn_live_rows(edges, p.emu_blocks, p.n_emu_blocks, p.emu_rows, ne, x, xdiv, x_nz,
+                              y, ldy, d, &ep, p.emu_live, st);
+    };
+    if (live) {
+        if (!sc) {
+            if (int e = layer_kernel(s)) return e;
+            return live_rows(s);
+        }
+        if (int e = mark(0, s)) return e;
+        if (int e = herr(hipEventRecord(sc->fork, s))) return e;
+        if (int e = herr(hipStreamWaitEvent(sc->aux[0], sc->fork, 0))) return e;
+        if (int e = live_rows(sc->aux[0])) return e;
+        if (int e = mark(4, sc->aux[0])) return e;
+        if (int e = layer_kernel(s)) return e;
+        if (int e = mark(3, s)) return e;
+        if (int e = herr(hipEventRecord(sc->join[0], sc->aux[0]))) return e;
+        if (int e = herr(hipStreamWaitEvent(s, sc->join[0], 0))) return e;
+        return mark(7, s);
+    }
     if (!sc || ne == 0) {
         for (int i = 0; i < 3; ++i)
             if (i < 2 || !chains)

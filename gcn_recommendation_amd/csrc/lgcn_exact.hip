@@ -932,13 +932,14 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     // (dma4 / dma16): its LDS reads are then ordinary, scheduled and counted by it, and the
     // explicit vmcnt waits (asm, "memory") keep them behind the data they read.
     static_assert(NX == AHEAD + 1 && NR == 2 * AHEAD + 1, "ring sizes");
+    float acc = 0.f;
+    if (nwin > 0) {  // (an empty row — live-edge rows may have none — reads no record)
     for (int w = 0; w < AHEAD; ++w) rec_dma(w);
     wait_vm<0>();
     for (int v = -AHEAD; v < 0; ++v) {
         x_dma(v + AHEAD);
         rec_dma(v + 2 * AHEAD);
     }
-    float acc = 0.f;
     const int cc = lane < W ? lane : 0;
     for (int32_t w = 0; w < nwin; ++w) {
         wait_vm<(AHEAD - 1) * (C::NI + 2)>();
@@ -991,6 +992,7 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
         }
     }
     wait_vm<0>();  // no LDS-DMA may land after the wave (and its LDS) is gone
+    }
     if (lane >= W || c0 + lane >= d) return;
     const int c = c0 + lane;
     const int32_t row = er.row;
@@ -1044,6 +1046,132 @@ int chain_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         default: return LGCN_EINVAL;
     }
 }
+// ---------------------------------------------------------------------------------------------
+// row-sparse X (the backward's first layer on a BPR batch's gradient): emulated rows as chains
+// over their LIVE edges only
+// ---------------------------------------------------------------------------------------------
+// An edge into an all-zero row of X adds fma(v, +-0, acc) == acc to the chain (v finite: the
+// chain value is unchanged, +0 stays +0), so the reference's chain over a row equals the chain
+// over its live edges in stored order. A BPR batch leaves a few thousand live rows of millions,
+// so a 2.77M-edge row keeps a few hundred live edges: compacted (three launches over the rows'
+// blocks, no host sync) they run as ordinary chain rows (k_chain_rows) — no block pass, no walk.
+// Edges with a non-finite value are kept (inf * 0 is NaN in the reference's chain too).
+//
+// Scratch layout (lgcn_live_scratch_bytes): int32 off[n_blocks] | lgcn_emu_row_t lrows[n_rows] |
+// lgcn_emu_block_t lblocks[n_rows] | lgcn_edge_t ledges[n_blocks * LGCN_EMU_BLOCK]; emulated row
+// i's live edges go to ledges[first_block_i * LGCN_EMU_BLOCK ...] (its blocks' own span).
+struct LiveScratch {
+    int32_t* off;
+    lgcn_emu_row_t* lrows;
+    lgcn_emu_block_t* lblocks;
+    lgcn_edge_t* ledges;
+};
+
+__host__ __device__ inline size_t live_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+__host__ __device__ inline LiveScratch live_layout(void* base, int32_t n_rows, int32_t n_blocks) {
+    char* p = static_cast<char*>(base);
+    LiveScratch s;
+    s.off = reinterpret_cast<int32_t*>(p);
+    p += live_align((size_t)n_blocks * 4);
+    s.lrows = reinterpret_cast<lgcn_emu_row_t*>(p);
+    p += live_align((size_t)n_rows * sizeof(lgcn_emu_row_t));
+    s.lblocks = reinterpret_cast<lgcn_emu_block_t*>(p);
+    p += live_align((size_t)n_rows * sizeof(lgcn_emu_block_t));
+    s.ledges = reinterpret_cast<lgcn_edge_t*>(p);
+    return s;
+}
+
+inline size_t live_bytes(int32_t n_rows, int32_t n_blocks) {
+    return live_align((size_t)n_blocks * 4) + live_align((size_t)n_rows * sizeof(lgcn_emu_row_t)) +
+           live_align((size_t)n_rows * sizeof(lgcn_emu_block_t)) +
+           (size_t)n_blocks * LGCN_EMU_BLOCK * sizeof(lgcn_edge_t);
+}
+
+// lane l's 4 edges of block b (steps 4l .. 4l+3): live flags (bit k) and the records
+__device__ __forceinline__ int live_flags(const lgcn_edge_t* __restrict__ edges,
+                                          const lgcn_emu_block_t& blk,
+                                          const uint32_t* __restrict__ x_nz, int2 (&rec)[4]) {
+    const int lane = threadIdx.x;
+    int f = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int32_t j = blk.beg + 4 * lane + k;
+        const bool in = j < blk.end;
+        rec[k] = *reinterpret_cast<const int2*>(edges + (in ? j : blk.beg));
+        const float v = __int_as_float(rec[k].y);
+        const bool live = in && (row_live_x(x_nz, rec[k].x) || !__builtin_isfinite(v));
+        f |= live ? (1 << k) : 0;
+    }
+    return f;
+}
+
+// per block: its live-edge count -> off[b]
+__global__ __launch_bounds__(64) void k_live_count(const lgcn_edge_t* __restrict__ edges,
+                                                   const lgcn_emu_block_t* __restrict__ blocks,
+                                                   const uint32_t* __restrict__ x_nz,
+                                                   int32_t* __restrict__ off) {
+    int2 rec[4];
+    const int f = live_flags(edges, blocks[blockIdx.x], x_nz, rec);
+    const int tot = wave_incl_scan(__builtin_popcount((unsigned)f));
+    if (threadIdx.x == 63) off[blockIdx.x] = tot;
+}
+
+// per emulated row (256 threads): exclusive scan of its blocks' counts in place, and the row's
+// descriptors of the compacted edges (one block per row, lgcn_chain_rows reads its span)
+__global__ __launch_bounds__(256) void k_live_scan(const lgcn_emu_row_t* __restrict__ rows,
+                                                   int32_t* __restrict__ off,
+                                                   lgcn_emu_row_t* __restrict__ lrows,
+                                                   lgcn_emu_block_t* __restrict__ lblocks) {
+    __shared__ int32_t s_wave[4];
+    __shared__ int32_t s_carry;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const lgcn_emu_row_t er = rows[blockIdx.x];
+    if (t == 0) s_carry = 0;
+    __syncthreads();
+    for (int32_t b0 = 0; b0 < er.n_blocks; b0 += 256) {
+        const int32_t b = b0 + t;
+        const int32_t c = b < er.n_blocks ? off[er.first_block + b] : 0;
+        const int incl = wave_incl_scan(c);
+        if (lane == 63) s_wave[w] = incl;
+        __syncthreads();
+        int base = s_carry;
+        for (int i = 0; i < w; ++i) base += s_wave[i];
+        const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        if (b < er.n_blocks) off[er.first_block + b] = base + incl - c;
+        __syncthreads();
+        if (t == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (t == 0) {
+        const int32_t beg = er.first_block * LGCN_EMU_BLOCK;
+        lrows[blockIdx.x] = lgcn_emu_row_t{er.row, (int32_t)blockIdx.x, 1, 0};
+        lblocks[blockIdx.x] = lgcn_emu_block_t{(int32_t)blockIdx.x, beg, beg + s_carry, 1};
+    }
+}
+
+// per block: its live edges, in stored order, to the row's compacted span
+__global__ __launch_bounds__(64) void k_live_scatter(const lgcn_edge_t* __restrict__ edges,
+                                                     const lgcn_emu_block_t* __restrict__ blocks,
+                                                     const lgcn_emu_row_t* __restrict__ rows,
+                                                     const uint32_t* __restrict__ x_nz,
+                                                     const int32_t* __restrict__ off,
+                                                     lgcn_edge_t* __restrict__ ledges) {
+    const lgcn_emu_block_t blk = blocks[blockIdx.x];
+    int2 rec[4];
+    const int f = live_flags(edges, blk, x_nz, rec);
+    const int cnt = __builtin_popcount((unsigned)f);
+    int pos = wave_incl_scan(cnt) - cnt;
+    const int64_t base = (int64_t)rows[blk.row].first_block * LGCN_EMU_BLOCK + off[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if ((f >> k) & 1) {
+            *reinterpret_cast<int2*>(ledges + base + pos) = rec[k];
+            ++pos;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1182,6 +1310,43 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         case LGCN_EPI_ADD: return chain_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
         default: return LGCN_EINVAL;
     }
+}
+
+}  // extern "C"
+
+extern "C" {
+
+size_t lgcn_live_scratch_bytes(int32_t n_rows, int32_t n_blocks) {
+    if (n_rows < 0 || n_blocks < 0) return 0;
+    return live_bytes(n_rows, n_blocks);
+}
+
+int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                   const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
+                   const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
+                   const lgcn_epilogue_t* epi_host, void* scratch, void* stream) {
+    if (n_rows < 0 || n_blocks < 0 || !lgcn_chain_supported(d) || d > 2048 || !x_nz ||
+        !(x_div > 0.f) || !epi_host)
+        return LGCN_EINVAL;
+    if (n_rows == 0) return 0;
+    if (!edges || !blocks || !rows || !y || !scratch || ldy < d || !x.p0 || n_blocks < n_rows)
+        return LGCN_EINVAL;
+    // compacted spans are indexed by first_block * LGCN_EMU_BLOCK in int32 edge offsets
+    if ((int64_t)n_blocks * LGCN_EMU_BLOCK > INT32_MAX) return LGCN_EINVAL;
+    if (reinterpret_cast<uintptr_t>(scratch) & 255) return LGCN_EALIGN;
+    const LiveScratch ls = live_layout(scratch, n_rows, n_blocks);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_live_count, dim3((uint32_t)n_blocks), dim3(64), 0, s, edges, blocks, x_nz,
+                       ls.off);
+    if (int e = herr_x(hipGetLastError())) return e;
+    hipLaunchKernelGGL(k_live_scan, dim3((uint32_t)n_rows), dim3(256), 0, s, rows, ls.off,
+                       ls.lrows, ls.lblocks);
+    if (int e = herr_x(hipGetLastError())) return e;
+    hipLaunchKernelGGL(k_live_scatter, dim3((uint32_t)n_blocks), dim3(64), 0, s, edges, blocks,
+                       rows, x_nz, ls.off, ls.ledges);
+    if (int e = herr_x(hipGetLastError())) return e;
+    return lgcn_chain_rows(ls.ledges, ls.lblocks, ls.lrows, n_rows, x, x_div, y, ldy, d, epi_host,
+                           stream);
 }
 
 }  // extern "C"

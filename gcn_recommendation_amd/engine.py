@@ -31,7 +31,7 @@ SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
-ABI_VERSION = 10
+ABI_VERSION = 11
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -116,7 +116,7 @@ class PlanT(ctypes.Structure):
                 ("n_rows", ctypes.c_int32), ("n_pre", ctypes.c_int32),
                 ("n_emu_blocks", ctypes.c_int32), ("n_emu_rows", ctypes.c_int32),
                 ("emu_part_rows", ctypes.c_int32 * 2), ("emu_part_blocks", ctypes.c_int32 * 2),
-                ("emu_scratch_blocks", ctypes.c_int32)]
+                ("emu_scratch_blocks", ctypes.c_int32), ("emu_live", ctypes.c_void_p)]
 
 
 class LgcnError(RuntimeError):
@@ -168,6 +168,9 @@ ABI = [
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
                                      _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P]),
     ("lgcn_chain_supported", ctypes.c_int, [_I32]),
+    ("lgcn_live_scratch_bytes", ctypes.c_size_t, [_I32, _I32]),
+    ("lgcn_live_rows", ctypes.c_int, [_P, _P, _I32, _P, _I32, RowsT, ctypes.c_float, _P, _P, _I64,
+                                      _I32, ctypes.POINTER(EpilogueT), _P, _P]),
     ("lgcn_chain_rows", ctypes.c_int, [_P, _P, _P, _I32, RowsT, ctypes.c_float, _P, _I64, _I32,
                                        ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_sched_create", ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_void_p)]),
@@ -331,6 +334,7 @@ class HubPlan:
         # host copy of the emulated rows' block counts (longest first): no device read-back
         self.emu_nb = np.zeros(0, np.int64) if emu_nb is None else np.asarray(emu_nb, np.int64)
         self._scratch = {}
+        self._live = None
         self._split = None
         self._split_bounds = None
 
@@ -386,18 +390,29 @@ class HubPlan:
             self._scratch[key] = (part, rel, meta, stage, n_blocks)
         return self._scratch[key][:4]
 
+    def live_scratch(self, device):
+        """Scratch of lgcn_live_rows (row-sparse X: the emulated rows as chains over their live
+        edges), allocated once per plan: n_emu_blocks x 2 KB of compacted edges + descriptors."""
+        if self._live is None and self.n_emu_rows:
+            nb = int(load_library().lgcn_live_scratch_bytes(self.n_emu_rows, self.n_emu_blocks))
+            self._live = torch.empty(nb, dtype=torch.uint8, device=device)
+        return self._live
+
     def release_scratch(self, d=None):
         """Drop the cached scratch of width d (all widths: None); torch.cuda.empty_cache() can
         then return it."""
         for key in list(self._scratch):
             if d is None or key[0] == d:
                 del self._scratch[key]
+        if d is None:
+            self._live = None
 
-    def struct(self, d, device, nnz=None, walk_all=False, scratch_set=0):
+    def struct(self, d, device, nnz=None, walk_all=False, scratch_set=0, live=False):
         """lgcn_hub_plan_t for width d. nnz: the operator's nonzeros (sets the chain/walk cut;
         None = every emulated row walked). walk_all: the chain rows are walked too (no chain
         kernel for this d / alignment, or LGCN_CHAIN=0), so the scratch covers every block.
-        scratch_set: which of the plan's scratch sets (0, 1) the layer uses."""
+        scratch_set: which of the plan's scratch sets (0, 1) the layer uses. live: attach the
+        live-edge scratch (a layer with a row-sparse X then runs lgcn_live_rows)."""
         if nnz is None or walk_all:
             rows = [self.n_emu_rows, self.n_emu_rows] if nnz is None else None
             blocks = [self.n_emu_blocks, self.n_emu_blocks] if nnz is None else None
@@ -420,6 +435,8 @@ class HubPlan:
         p.emu_part_rows[0], p.emu_part_rows[1] = rows
         p.emu_part_blocks[0], p.emu_part_blocks[1] = blocks
         p.emu_scratch_blocks = need
+        lv = self.live_scratch(device) if live and self.mode == "exact" else None
+        p.emu_live = lv.data_ptr() if lv is not None else None
         return p
 
 
@@ -936,7 +953,8 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     if main.cuda_stream != (stream.value or 0):
         raise LgcnError("spmm_layer: stream must be the device's current stream")
     chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
-    plan = hp.struct(d, graph.device, nnz=graph.nnz, walk_all=not chains)
+    plan = hp.struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
+                     live=x_nz is not None and live_enabled())
     x = rows_desc(x_segments, d)
     sc = sched_for(graph.device) if hp.n_emu_rows else None
     args = (_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), graph.n_rows)
@@ -971,8 +989,15 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
     return y
 
 
-def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned):
-    """The 4 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * side + set]."""
+def live_enabled():
+    """LGCN_LIVE=0 turns off the live-edge chains of a row-sparse X (lgcn_live_rows): the
+    emulated rows are then block-passed and walked over all their edges (same bits)."""
+    return os.environ.get("LGCN_LIVE", "1") != "0"
+
+
+def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=False):
+    """The 4 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * side + set]. live: attach the
+    live-edge scratch (the backward of a row-sparse G)."""
     lib = load_library()
     hps = graph.side_hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
     chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and xs_aligned
@@ -980,7 +1005,7 @@ def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned):
     for side in (0, 1):
         for j in (0, 1):
             arr[2 * side + j] = hps[side].struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
-                                                 scratch_set=j)
+                                                 scratch_set=j, live=live and live_enabled())
     return arr, hps
 
 
@@ -1159,7 +1184,8 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
             nz, _ = rows_nonzero(segs, d, dev)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
         if use_sides(gt):
-            plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs))
+            plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
+                                   live=nz is not None)
             sc = sched_for(dev)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             try:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 10
+#define LGCN_ABI_VERSION 11
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -161,6 +161,10 @@ typedef struct {
     int32_t emu_part_rows[2];
     int32_t emu_part_blocks[2];
     int32_t emu_scratch_blocks;
+    /* optional (NULL = off) scratch of lgcn_live_scratch_bytes(n_emu_rows, n_emu_blocks) bytes,
+     * 256-B aligned: with a row-sparse X (x_nz) every emulated row runs as a chain over its live
+     * edges (lgcn_live_rows) instead of block pass + walk / chain over all of them */
+    void* emu_live;
 } lgcn_hub_plan_t;
 
 /* Host planner of an exact hub plan (host memory only, no GPU call): from the host row pointers
@@ -374,6 +378,19 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                     const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
                     float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
                     void* stream);
+
+/* Row-sparse X (x_nz from lgcn_rows_nonzero: the backward's first layer on a BPR batch's
+ * gradient): an edge into an all-zero row adds fma(v, +-0, acc) == acc to the reference's chain,
+ * so each emulated row's chain equals the chain over its LIVE edges in stored order (edges with a
+ * non-finite value are kept). lgcn_live_rows compacts them on the device (no host sync) into
+ * scratch (lgcn_live_scratch_bytes, 256-B aligned) and runs them as lgcn_chain_rows; a 2.77M-edge
+ * row keeps a few hundred. rows / blocks: the plan's emulated rows (lgcn_plan_exact). d and X as
+ * for lgcn_chain_rows. */
+size_t lgcn_live_scratch_bytes(int32_t n_rows, int32_t n_blocks);
+int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                   const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
+                   const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
+                   const lgcn_epilogue_t* epi_host, void* scratch, void* stream);
 
 /* Concurrent schedule of the exact layers (lgcn_layer, lgcn_propagate_forward/backward): the
  * emulated and chain rows run on auxiliary streams beside the layer kernel, forked from and

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 10
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 11
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -105,7 +105,15 @@ def test_argument_validation_without_gpu(lib):
                                None) == 0     # nothing to do
     assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 24, ctypes.byref(ep),
                                None) == -1    # unsupported width
-    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4  # (+ tail padding)
+    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8  # (+ padding, emu_live)
+    # live-edge rows: the row mask and the scratch are required, widths as the chain kernel's
+    assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, None, None, 64, 64,
+                              ctypes.byref(ep), ctypes.c_void_p(256), None) == -1   # no x_nz
+    assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, ctypes.c_void_p(8), None, 64, 24,
+                              ctypes.byref(ep), ctypes.c_void_p(256), None) == -1   # width
+    assert lib.lgcn_live_rows(None, None, 0, None, 0, rows, 1.0, ctypes.c_void_p(8), None, 64, 64,
+                              ctypes.byref(ep), None, None) == 0   # nothing to do
+    assert lib.lgcn_live_scratch_bytes(3, 10) >= 10 * 256 * 8 + 10 * 4 + 3 * 32
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,
                                   ctypes.byref(nbytes), None) == -1
@@ -142,7 +150,8 @@ def test_struct_layout_matches_header():
 int main(void){
  printf("%zu %zu %zu %zu\n", sizeof(lgcn_rows_t), sizeof(lgcn_epilogue_t),
         sizeof(lgcn_hub_item_t), sizeof(lgcn_hub_row_t));
- printf("%zu %zu %zu %zu %zu\n", offsetof(lgcn_epilogue_t, prev0),
+ printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(lgcn_hub_plan_t),
+        offsetof(lgcn_hub_plan_t, emu_live), offsetof(lgcn_epilogue_t, prev0),
         offsetof(lgcn_epilogue_t, prev_dense), offsetof(lgcn_epilogue_t, ld_prev),
         offsetof(lgcn_epilogue_t, addend), offsetof(lgcn_epilogue_t, addend_nz));
  return 0;}
@@ -157,8 +166,8 @@ int main(void){
     offs = [int(x) for x in l2.split()]
     assert sizes == [ctypes.sizeof(engine.RowsT), ctypes.sizeof(engine.EpilogueT), 16, 16]
     E = engine.EpilogueT
-    assert offs == [E.prev0.offset, E.prev_dense.offset, E.ld_prev.offset, E.addend.offset,
-                    E.addend_nz.offset]
+    assert offs == [ctypes.sizeof(engine.PlanT), engine.PlanT.emu_live.offset, E.prev0.offset,
+                    E.prev_dense.offset, E.ld_prev.offset, E.addend.offset, E.addend_nz.offset]
 
 
 def test_engine_refuses_missing_library(tmp_path):

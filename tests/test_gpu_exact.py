@@ -126,3 +126,38 @@ def test_exact_is_default_and_deterministic(gpu_device, monkeypatch):
     b = engine.propagate_forward(g, x, 3).cpu().numpy()
     assert g.hubs(engine.hub_threshold_from_env()).n_emu_rows > 0
     assert np.array_equal(a, b) and np.array_equal(a, oracle.forward(r, c, v, e0, 3))
+
+
+@pytest.mark.parametrize("sides", [False, True])
+def test_live_edge_chains_bpr_gradient(gpu_device, monkeypatch, sides):
+    """The backward of a BPR batch's gradient (a few live rows): every emulated row of the first
+    layer runs as a chain over its live edges (lgcn_live_rows: device compaction + chain kernel),
+    bitwise the oracle's full chain — on a 300k-edge item row and power-law hubs, rows with no
+    live edge at all included, on one operator and on the bipartite two-lane schedule."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "1")
+    rng = np.random.default_rng(21)
+    U, I = 300_000, 3_000
+    users = np.concatenate([np.arange(U), rng.integers(0, U, 200_000)])
+    p = 1.0 / np.arange(1, I) ** 1.1
+    items = np.concatenate([np.zeros(U, np.int64), 1 + rng.choice(I - 1, 200_000, p=p / p.sum())])
+    r, c, v, n = oracle.build_norm_adj(users, items, U, I, 0, use_brand=False)
+    adj = _adj(r, c, v, n, gpu_device)
+    g = engine.graph_from_coo(adj, sides=(U, U + I) if sides else None)
+    assert (g.split is not None) == sides
+    d, K = 64, 3
+    G = np.zeros((n, d), np.float32)
+    live_u = rng.integers(0, U, 2048)
+    live_i = U + rng.integers(0, I, 4096)
+    G[live_u] = rng.standard_normal((live_u.size, d)).astype(np.float32) * 1e-3
+    G[live_i] = rng.standard_normal((live_i.size, d)).astype(np.float32) * 1e-3
+    want = oracle.backward(r, c, v, G, K)
+    gt = torch.from_numpy(G).to(gpu_device)
+    kw = dict(hub_threshold=128, hub_mode="exact")
+    got = engine.propagate_backward(g, gt, K, sparse="on", **kw).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    monkeypatch.setenv("LGCN_LIVE", "0")
+    got0 = engine.propagate_backward(g, gt, K, sparse="on", **kw).cpu().numpy()
+    assert np.array_equal(got0.view(np.uint32), want.view(np.uint32))
+    # an all-zero gradient: every live-edge row is empty
+    z = engine.propagate_backward(g, torch.zeros_like(gt), K, sparse="on", **kw)
+    assert not bool(z.any())
