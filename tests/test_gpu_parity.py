@@ -258,7 +258,7 @@ def test_c_abi_whole_forward_backward(gpu_device, monkeypatch, order, mode):
     # same lgcn_layer schedule engine.spmm_layer runs); then again in order on one stream
     plan = hp.struct(d, gpu_device, nnz=g.nnz)
     sched = engine.sched_for(gpu_device)
-    assert sched is not None and sched.n_aux == 3
+    assert sched is not None and sched.n_aux in (3, 7)  # 7: GPU_MAX_HW_QUEUES >= 8
     layers = [torch.empty((n, d), device=gpu_device) for _ in range(K - 1)]
     out = torch.empty((n, d), device=gpu_device)
     bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
