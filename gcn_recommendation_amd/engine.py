@@ -894,6 +894,16 @@ class Sched:
             pass
 
 
+def _capture_aux(device):
+    """Auxiliary streams while the caller's stream is being captured into a HIP graph: at most 3
+    (one lane). The two-lane schedule's 8 streams forked and joined inside one capture crash
+    hipStreamEndCapture on this ROCm (segfault, tests/test_gpu_sides.py), so a captured sided
+    propagation runs its half-layers in order on one lane — same kernels, same bits."""
+    if torch.cuda.is_current_stream_capturing():
+        return min(3, n_aux_streams())
+    return None
+
+
 def sched_for(device, n_aux=None):
     """The device's Sched (None with LGCN_EMU_OVERLAP=0: every part in order on the caller's
     stream). n_aux: default n_aux_streams()."""
@@ -902,6 +912,8 @@ def sched_for(device, n_aux=None):
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled())
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
+        if key[1] > 3:  # the one-lane schedule a capture falls back to, made outside any capture
+            sched_for(device, 3)
     return _scheds[key]
 
 
@@ -1092,7 +1104,7 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
         if use_sides(graph, layer_events, kernel_events):
             plans, _ = _side_plans(graph, d, hub_threshold, hub_mode, emu_min,
                                    _aligned16(segments))
-            sc = sched_for(dev)
+            sc = sched_for(dev, _capture_aux(dev))
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
             try:
@@ -1186,7 +1198,7 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         if use_sides(gt):
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
                                    live=nz is not None)
-            sc = sched_for(dev)
+            sc = sched_for(dev, _capture_aux(dev))
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             try:
                 _check(lib.lgcn_propagate_backward_sides(
