@@ -808,22 +808,28 @@ struct EmuPart {
 
 // rows [r0, r1) of the emulated-row list: block pass (blocks [b0, b1)) into the scratch at the
 // part's block offset
+// live: NULL, or lgcn_live_rows' per-row flags over the whole emulated-row list (rows the
+// live-edge chains ran are skipped)
 int part_blocks(const lgcn_edge_t* edges, const lgcn_hub_plan_t& p, const EmuPart& q,
-                const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, hipStream_t s) {
+                const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d,
+                const lgcn_emu_row_t* live, hipStream_t s) {
     if (q.b1 <= q.b0) return 0;
     const int64_t b0 = q.b0;
     return lgcn_emu_blocks(edges, p.emu_blocks + b0, q.b1 - q.b0, x, xdiv, x_nz, d,
                            p.emu_rel + b0 * d * LGCN_EMU_CANDS,
                            static_cast<char*>(p.emu_meta) + b0 * d * LGCN_EMU_META_BYTES,
-                           p.emu_stage ? p.emu_stage + b0 * (d + 1) * LGCN_EMU_BLOCK : nullptr, s);
+                           p.emu_stage ? p.emu_stage + b0 * (d + 1) * LGCN_EMU_BLOCK : nullptr,
+                           live, s);
 }
 
 int part_walk(const lgcn_edge_t* edges, const lgcn_hub_plan_t& p, const EmuPart& q,
               const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y, int64_t ldy,
-              int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
+              int32_t d, const lgcn_epilogue_t& ep, int slots, const lgcn_emu_row_t* live,
+              hipStream_t s) {
     if (q.r1 <= q.r0) return 0;
     return lgcn_emu_walk(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, p.emu_rel,
-                         p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, slots, s);
+                         p.emu_meta, p.emu_stage, x, xdiv, x_nz, y, ldy, d, &ep, slots,
+                         live ? live + q.r0 : nullptr, s);
 }
 
 bool chain_ok(const lgcn_rows_t& x, int32_t d) {
@@ -849,7 +855,7 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     const bool live = x_nz && p.emu_live && ne > 0 && chain_ok(x, d) && (!sc || sc->chain);
     const bool chains = !live && ne > p.emu_part_rows[1] && chain_ok(x, d) && (!sc || sc->chain);
     // walked rows read the block-pass scratch, which must cover their blocks
-    if (!live && (chains ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
+    if ((chains || live ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
         return LGCN_EINVAL;
     hipEvent_t* tr = sc ? sc->trace : nullptr;
     auto mark = [&](int k, hipStream_t st) -> int {
@@ -878,34 +884,60 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
         return lgcn_chain_rows(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, x, xdiv, y,
                                ldy, d, &ep, st);
     };
+    // live path: the live-edge chains take every chain row (part 2) and every walked row with at
+    // most LGCN_LIVE_MAX live edges; block pass + walk run the rest (their waves of the live
+    // rows exit at once). Dense X: every walked row stays walked, the chains cover part 2.
+    const lgcn_emu_row_t* lflags =
+        live ? lgcn_live_flags(p.emu_live, ne, p.n_emu_blocks) : nullptr;
     auto live_rows = [&](hipStream_t st) -> int {
         return lgcn_live_rows(edges, p.emu_blocks, p.n_emu_blocks, p.emu_rows, ne, x, xdiv, x_nz,
-                              y, ldy, d, &ep, p.emu_live, st);
+                              y, ldy, d, &ep, p.emu_part_rows[1], LGCN_LIVE_MAX, p.emu_live, st);
+    };
+    auto walked = [&](int i, hipStream_t st) -> int {
+        if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, lflags, st)) return e;
+        return part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i], lflags, st);
     };
     if (live) {
         if (!sc) {
-            if (int e = layer_kernel(s)) return e;
-            return live_rows(s);
+            if (int e = live_rows(s)) return e;
+            for (int i = 0; i < 2; ++i)
+                if (int e = walked(i, s)) return e;
+            return layer_kernel(s);
         }
+        // aux[0]: the live-edge pass (its row flags gate the walks), then part 0's walk; aux[1]
+        // (after the flags): part 1
+        const int na = sc->n_aux;
+        hipStream_t a0 = sc->aux[0], a1 = sc->aux[na > 1 ? 1 : 0];
         if (int e = mark(0, s)) return e;
         if (int e = herr(hipEventRecord(sc->fork, s))) return e;
-        if (int e = herr(hipStreamWaitEvent(sc->aux[0], sc->fork, 0))) return e;
-        if (int e = live_rows(sc->aux[0])) return e;
-        if (int e = mark(4, sc->aux[0])) return e;
+        if (int e = herr(hipStreamWaitEvent(a0, sc->fork, 0))) return e;
+        if (int e = live_rows(a0)) return e;
+        if (int e = mark(4, a0)) return e;
+        if (a1 != a0) {
+            if (int e = herr(hipEventRecord(sc->join[0], a0))) return e;
+            if (int e = herr(hipStreamWaitEvent(a1, sc->join[0], 0))) return e;
+        }
+        if (int e = walked(0, a0)) return e;
+        if (int e = mark(5, a0)) return e;
+        if (int e = walked(1, a1)) return e;
+        if (int e = mark(6, a1)) return e;
         if (int e = layer_kernel(s)) return e;
         if (int e = mark(3, s)) return e;
-        if (int e = herr(hipEventRecord(sc->join[0], sc->aux[0]))) return e;
-        if (int e = herr(hipStreamWaitEvent(s, sc->join[0], 0))) return e;
+        for (int i = 0; i < (a1 != a0 ? 2 : 1); ++i) {
+            if (int e = herr(hipEventRecord(sc->join[i], sc->aux[i]))) return e;
+            if (int e = herr(hipStreamWaitEvent(s, sc->join[i], 0))) return e;
+        }
         return mark(7, s);
     }
     if (!sc || ne == 0) {
         for (int i = 0; i < 3; ++i)
             if (i < 2 || !chains)
-                if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, s)) return e;
+                if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, nullptr, s)) return e;
         if (int e = layer_kernel(s)) return e;
         for (int i = 0; i < 3; ++i)
             if (i < 2 || !chains)
-                if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i], s))
+                if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
+                                      nullptr, s))
                     return e;
         return chains ? chain_rows(s) : 0;
     }
@@ -920,7 +952,8 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     // kernel, then the walks and the chains
     for (int i = 0; i < 3; ++i)
         if (i < 2 || !chains) {
-            if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, aux_of(i))) return e;
+            if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, nullptr, aux_of(i)))
+                return e;
             if (i < 2)
                 if (int e = mark(1 + i, aux_of(i))) return e;
         }
@@ -933,7 +966,7 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     for (int i = 0; i < 3; ++i)
         if (i < 2 || !chains) {
             if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
-                                  aux_of(i)))
+                                  nullptr, aux_of(i)))
                 return e;
             if (i < 2)
                 if (int e = mark(5 + i, aux_of(i))) return e;

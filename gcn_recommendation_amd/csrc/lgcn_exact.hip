@@ -129,12 +129,15 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                                                    const uint32_t* __restrict__ x_nz, int32_t d,
                                                    int4* __restrict__ ktab,
                                                    int4* __restrict__ meta,
-                                                   float* __restrict__ stage) {
+                                                   float* __restrict__ stage,
+                                                   const lgcn_emu_row_t* __restrict__ live) {
     constexpr int SW = 16;  // steps gathered per sub-window (all in flight at once)
     const int lane = threadIdx.x;
     const int c = blockIdx.y * 64 + lane;
     const bool act = c < d;
     const lgcn_emu_block_t blk = blocks[blockIdx.x];
+    // a row the live-edge chains run (lgcn_live_rows flags it) needs no block pass
+    if (live && live[blk.row].n_blocks) return;
     // T: the sequential fma chain of the block from +0. It is the true chain for block 0; for
     // every block it tracks the exact running sum S of the products to within 1/2 ulp(|T|) per
     // step, which bounds every trajectory of the block (meta lo0/hi0)
@@ -499,7 +502,8 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                                                  const float* __restrict__ stage, lgcn_rows_t x,
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
-                                                 lgcn_epilogue_t ep, int NS, int max_it) {
+                                                 lgcn_epilogue_t ep, int NS, int max_it,
+                                                 const lgcn_emu_row_t* __restrict__ live) {
     constexpr int CH = LGCN_EMU_CH;
     constexpr int B = LGCN_EMU_BLOCK;
     static_assert(CH == 64, "one lane per block of a chunk");
@@ -516,6 +520,8 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // issue priority over the co-resident waves of other kernels on this SIMD (build flag A/B)
     __builtin_amdgcn_s_setprio(LGCN_WALK_PRIO);
 #endif
+    // a row the live-edge chains run (lgcn_live_rows flags it, aligned with `rows`) is theirs
+    if (live && live[blockIdx.x].n_blocks) return;
     const lgcn_emu_row_t er = rows[blockIdx.x];
     const int64_t fb = er.first_block;
     const int nb_all = er.n_blocks;
@@ -795,10 +801,10 @@ bool is_pow2(float x) {
 template <int XD>
 int launch_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                   const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, int4* ktab,
-                  int4* meta, float* stage, hipStream_t s) {
+                  int4* meta, float* stage, const lgcn_emu_row_t* live, hipStream_t s) {
     const dim3 grid((uint32_t)n_blocks, (uint32_t)((d + 63) / 64));
     hipLaunchKernelGGL((k_emu_blocks<XD>), grid, dim3(64), 0, s, edges, blocks, x, xdiv, x_nz, d,
-                       ktab, meta, stage);
+                       ktab, meta, stage, live);
     return herr_x(hipGetLastError());
 }
 
@@ -806,7 +812,8 @@ template <int MODE, int XD>
 int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                 const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
                 const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
-                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
+                int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
+                const lgcn_emu_row_t* live, hipStream_t s) {
     const dim3 grid((uint32_t)n_rows, (uint32_t)d);
     const size_t lds = (size_t)(2 * slots + 1) * 2 * LGCN_EMU_BLOCK * sizeof(float);
     if (lds > 56 * 1024) {  // beyond the default dynamic-LDS limit: raise it once per kernel
@@ -816,7 +823,8 @@ int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         if (once != hipSuccess) return (int)once;
     }
     hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, ktab,
-                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots, lgcn_detail::g_emu_resolve);
+                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots, lgcn_detail::g_emu_resolve,
+                       live);
     return herr_x(hipGetLastError());
 }
 
@@ -828,9 +836,10 @@ template <int MODE>
 int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
               const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
               const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
-              int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots, hipStream_t s) {
+              int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
+              const lgcn_emu_row_t* live, hipStream_t s) {
 #define LGCN_W(XD_) \
-    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, s);
+    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, live, s);
     switch (xd) {
         LGCN_W(0) LGCN_W(1) LGCN_W(2) LGCN_W(4) LGCN_W(5) LGCN_W(6)
         default: return LGCN_EINVAL;
@@ -893,6 +902,7 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     const int lane = threadIdx.x;
     const int c0 = blockIdx.y * W;
     const lgcn_emu_row_t er = rows[blockIdx.x];
+    if (er.n_blocks <= 0) return;  // (a live-edge row left to the walk: lgcn_live_rows)
     const int32_t beg = blocks[er.first_block].beg;
     const int32_t end = blocks[er.first_block + er.n_blocks - 1].end;
     const int32_t nwin = (end - beg + 63) >> 6;
@@ -1122,7 +1132,8 @@ __global__ __launch_bounds__(64) void k_live_count(const lgcn_edge_t* __restrict
 __global__ __launch_bounds__(256) void k_live_scan(const lgcn_emu_row_t* __restrict__ rows,
                                                    int32_t* __restrict__ off,
                                                    lgcn_emu_row_t* __restrict__ lrows,
-                                                   lgcn_emu_block_t* __restrict__ lblocks) {
+                                                   lgcn_emu_block_t* __restrict__ lblocks,
+                                                   int32_t live_min, int32_t max_live) {
     __shared__ int32_t s_wave[4];
     __shared__ int32_t s_carry;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1145,7 +1156,13 @@ __global__ __launch_bounds__(256) void k_live_scan(const lgcn_emu_row_t* __restr
     }
     if (t == 0) {
         const int32_t beg = er.first_block * LGCN_EMU_BLOCK;
-        lrows[blockIdx.x] = lgcn_emu_row_t{er.row, (int32_t)blockIdx.x, 1, 0};
+        // n_blocks = 1: the live-edge chain runs the row; 0: left to the caller (block pass +
+        // walk skip the rows flagged 1)
+        // (a walk costs ~0.45 us per block, a chain ~1.2 us per 64 edges: 16 live edges per
+        // block is where the chain stops paying)
+        const bool mine = (int32_t)blockIdx.x >= live_min ||
+                          (int64_t)s_carry <= min((int64_t)max_live, (int64_t)er.n_blocks * 16);
+        lrows[blockIdx.x] = lgcn_emu_row_t{er.row, (int32_t)blockIdx.x, mine ? 1 : 0, 0};
         lblocks[blockIdx.x] = lgcn_emu_block_t{(int32_t)blockIdx.x, beg, beg + s_carry, 1};
     }
 }
@@ -1156,8 +1173,10 @@ __global__ __launch_bounds__(64) void k_live_scatter(const lgcn_edge_t* __restri
                                                      const lgcn_emu_row_t* __restrict__ rows,
                                                      const uint32_t* __restrict__ x_nz,
                                                      const int32_t* __restrict__ off,
+                                                     const lgcn_emu_row_t* __restrict__ lrows,
                                                      lgcn_edge_t* __restrict__ ledges) {
     const lgcn_emu_block_t blk = blocks[blockIdx.x];
+    if (!lrows[blk.row].n_blocks) return;  // the walk's row
     int2 rec[4];
     const int f = live_flags(edges, blk, x_nz, rec);
     const int cnt = __builtin_popcount((unsigned)f);
@@ -1210,7 +1229,7 @@ int lgcn_emu_row_stats(unsigned long long* out_host) {  // [256][4], then reset
 
 int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                     lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
-                    void* meta, float* stage, void* stream) {
+                    void* meta, float* stage, const lgcn_emu_row_t* live, void* stream) {
     if (n_blocks < 0 || d < 1 || d > 2048 || !(x_div > 0.f)) return LGCN_EINVAL;
     if (n_blocks == 0) return 0;
     if (!edges || !blocks || !rel || !meta || !x.p0) return LGCN_EINVAL;
@@ -1223,7 +1242,7 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
     int4* mp = static_cast<int4*>(meta);
     int4* kp = reinterpret_cast<int4*>(rel);
 #define LGCN_B(XD_) \
-    case XD_: return launch_blocks<XD_>(edges, blocks, n_blocks, x, xa, x_nz, d, kp, mp, stage, s);
+    case XD_: return launch_blocks<XD_>(edges, blocks, n_blocks, x, xa, x_nz, d, kp, mp, stage, live, s);
     switch (xd) {
         LGCN_B(0) LGCN_B(1) LGCN_B(2) LGCN_B(4) LGCN_B(5) LGCN_B(6)
         default: return LGCN_EINVAL;
@@ -1235,7 +1254,7 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
-                  void* stream) {
+                  const lgcn_emu_row_t* live, void* stream) {
     if (slots == 0) slots = LGCN_EMU_SLOTS;
     // static LDS (two translation tables, 8 KB) + (2 slots + 1) x 2 KB within 64 KB
     if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host || slots < 1 ||
@@ -1265,11 +1284,11 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     const int4* kp = reinterpret_cast<const int4*>(rel);
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
+            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         case LGCN_EPI_MEAN:
-            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
+            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         case LGCN_EPI_ADD:
-            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, s);
+            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         default:
             return LGCN_EINVAL;
     }
@@ -1321,10 +1340,16 @@ size_t lgcn_live_scratch_bytes(int32_t n_rows, int32_t n_blocks) {
     return live_bytes(n_rows, n_blocks);
 }
 
+const lgcn_emu_row_t* lgcn_live_flags(const void* scratch, int32_t n_rows, int32_t n_blocks) {
+    if (!scratch || n_rows < 0 || n_blocks < 0) return nullptr;
+    return live_layout(const_cast<void*>(scratch), n_rows, n_blocks).lrows;
+}
+
 int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                    const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
                    const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
-                   const lgcn_epilogue_t* epi_host, void* scratch, void* stream) {
+                   const lgcn_epilogue_t* epi_host, int32_t live_min, int32_t max_live,
+                   void* scratch, void* stream) {
     if (n_rows < 0 || n_blocks < 0 || !lgcn_chain_supported(d) || d > 2048 || !x_nz ||
         !(x_div > 0.f) || !epi_host)
         return LGCN_EINVAL;
@@ -1340,10 +1365,10 @@ int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int
                        ls.off);
     if (int e = herr_x(hipGetLastError())) return e;
     hipLaunchKernelGGL(k_live_scan, dim3((uint32_t)n_rows), dim3(256), 0, s, rows, ls.off,
-                       ls.lrows, ls.lblocks);
+                       ls.lrows, ls.lblocks, live_min, max_live);
     if (int e = herr_x(hipGetLastError())) return e;
     hipLaunchKernelGGL(k_live_scatter, dim3((uint32_t)n_blocks), dim3(64), 0, s, edges, blocks,
-                       rows, x_nz, ls.off, ls.ledges);
+                       rows, x_nz, ls.off, ls.lrows, ls.ledges);
     if (int e = herr_x(hipGetLastError())) return e;
     return lgcn_chain_rows(ls.ledges, ls.lblocks, ls.lrows, n_rows, x, x_div, y, ldy, d, epi_host,
                            stream);

@@ -164,13 +164,14 @@ ABI = [
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
     ("lgcn_emu_blocks", ctypes.c_int, [_P, _P, _I32, RowsT, ctypes.c_float, _P, _I32, _P, _P, _P,
-                                       _P]),
+                                       _P, _P]),
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
-                                     _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P]),
+                                     _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P, _P]),
     ("lgcn_chain_supported", ctypes.c_int, [_I32]),
     ("lgcn_live_scratch_bytes", ctypes.c_size_t, [_I32, _I32]),
     ("lgcn_live_rows", ctypes.c_int, [_P, _P, _I32, _P, _I32, RowsT, ctypes.c_float, _P, _P, _I64,
-                                      _I32, ctypes.POINTER(EpilogueT), _P, _P]),
+                                      _I32, ctypes.POINTER(EpilogueT), _I32, _I32, _P, _P]),
+    ("lgcn_live_flags", ctypes.c_void_p, [_P, _I32, _I32]),
     ("lgcn_chain_rows", ctypes.c_int, [_P, _P, _P, _I32, RowsT, ctypes.c_float, _P, _I64, _I32,
                                        ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_sched_create", ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_void_p)]),

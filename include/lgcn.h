@@ -350,13 +350,16 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
 
 /* Emulation block pass for one layer: for every block of every emulated row, candidate chains
  * + bounds over X (read as lgcn_spmm_layer reads it: x_div, x_nz) into rel / meta, and (stage
- * != NULL) the block's X elements per column into stage. */
+ * != NULL) the block's X elements per column into stage. live: NULL, or lgcn_live_flags() of a
+ * preceding lgcn_live_rows over the plan's whole emulated-row list — blocks of the rows it ran
+ * (flag n_blocks != 0, indexed by the block's `row`) are skipped. */
 int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                     lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
-                    void* meta, float* stage, void* stream);
+                    void* meta, float* stage, const lgcn_emu_row_t* live, void* stream);
 
 /* Emulation walk: each emulated row's final value per column (bitwise the sequential chain),
- * epilogue applied, written to Y. Needs lgcn_emu_blocks' rel / meta (and stage, if it wrote
+ * epilogue applied, written to Y. live: NULL, or the live-edge flags aligned with `rows` (rows
+ * flagged n_blocks != 0 are skipped: lgcn_live_rows wrote them). Needs lgcn_emu_blocks' rel / meta (and stage, if it wrote
  * one; NULL = blocks to resolve gather X) of the same X. slots: LDS slots per 64-block chunk
  * for the blocks predicted to need an in-block resolve, 1..LGCN_EMU_MAX_WALK_SLOTS (0 = the
  * default, 12): 4 KB of LDS per wave each (two chunks in flight), so a walk over short rows
@@ -365,7 +368,7 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
-                  void* stream);
+                  const lgcn_emu_row_t* live, void* stream);
 
 /* Mid-size emulated rows run as the reference's sequential chain itself (no block pass): one
  * wave per (row, column slice) folds acc = fma(val_j, X[col_j, c], acc) in stored order from +0
@@ -386,11 +389,18 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
  * scratch (lgcn_live_scratch_bytes, 256-B aligned) and runs them as lgcn_chain_rows; a 2.77M-edge
  * row keeps a few hundred. rows / blocks: the plan's emulated rows (lgcn_plan_exact). d and X as
  * for lgcn_chain_rows. */
+#define LGCN_LIVE_MAX 65536  /* a walked row with more live edges than this stays walked */
 size_t lgcn_live_scratch_bytes(int32_t n_rows, int32_t n_blocks);
+/* Rows [live_min, n_rows) are always run as live-edge chains, rows below live_min only when
+ * they hold at most max_live live edges (a dense X keeps the long rows on block pass + walk);
+ * lgcn_live_flags(scratch, ...) then marks per row (n_blocks != 0) the rows it ran — pass it to
+ * lgcn_emu_blocks / lgcn_emu_walk so they skip those. */
 int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                    const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,
                    const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
-                   const lgcn_epilogue_t* epi_host, void* scratch, void* stream);
+                   const lgcn_epilogue_t* epi_host, int32_t live_min, int32_t max_live,
+                   void* scratch, void* stream);
+const lgcn_emu_row_t* lgcn_live_flags(const void* scratch, int32_t n_rows, int32_t n_blocks);
 
 /* Concurrent schedule of the exact layers (lgcn_layer, lgcn_propagate_forward/backward): the
  * emulated and chain rows run on auxiliary streams beside the layer kernel, forked from and

@@ -93,12 +93,14 @@ def test_argument_validation_without_gpu(lib):
     assert lib.lgcn_sched_create(arr, 0, ctypes.byref(h)) == -1
     assert lib.lgcn_sched_set(None, engine.SCHED_SLOTS0, 4) == -1
     assert lib.lgcn_sched_destroy(None) == 0
-    assert lib.lgcn_emu_blocks(None, None, -1, rows, 1.0, None, 64, None, None, None, None) == -1
-    assert lib.lgcn_emu_blocks(None, None, 0, rows, 1.0, None, 64, None, None, None, None) == 0
+    assert lib.lgcn_emu_blocks(None, None, -1, rows, 1.0, None, 64, None, None, None, None,
+                               None) == -1
+    assert lib.lgcn_emu_blocks(None, None, 0, rows, 1.0, None, 64, None, None, None, None,
+                               None) == 0
     assert lib.lgcn_emu_walk(None, None, None, 2, None, None, None, rows, 1.0, None, None, 64, 64,
-                             ctypes.byref(ep), 0, None) == -1
+                             ctypes.byref(ep), 0, None, None) == -1
     assert lib.lgcn_emu_walk(None, None, None, 0, None, None, None, rows, 1.0, None, None, 64, 64,
-                             ctypes.byref(ep), 64, None) == -1   # slots out of range
+                             ctypes.byref(ep), 64, None, None) == -1   # slots out of range
     assert [lib.lgcn_chain_supported(d) for d in (8, 16, 24, 32, 64, 128, 192, 256)] == \
         [0, 1, 0, 1, 1, 1, 1, 1]
     assert lib.lgcn_chain_rows(None, None, None, 0, rows, 1.0, None, 64, 64, ctypes.byref(ep),
@@ -108,11 +110,11 @@ def test_argument_validation_without_gpu(lib):
     assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8  # (+ padding, emu_live)
     # live-edge rows: the row mask and the scratch are required, widths as the chain kernel's
     assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, None, None, 64, 64,
-                              ctypes.byref(ep), ctypes.c_void_p(256), None) == -1   # no x_nz
+                              ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # no x_nz
     assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, ctypes.c_void_p(8), None, 64, 24,
-                              ctypes.byref(ep), ctypes.c_void_p(256), None) == -1   # width
+                              ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # width
     assert lib.lgcn_live_rows(None, None, 0, None, 0, rows, 1.0, ctypes.c_void_p(8), None, 64, 64,
-                              ctypes.byref(ep), None, None) == 0   # nothing to do
+                              ctypes.byref(ep), 0, 0, None, None) == 0   # nothing to do
     assert lib.lgcn_live_scratch_bytes(3, 10) >= 10 * 256 * 8 + 10 * 4 + 3 * 32
     nbytes = ctypes.c_size_t(0)
     assert lib.lgcn_coo_sort_perm(None, -5, 10, None, None, None, None, None,

@@ -80,7 +80,7 @@ def main():
                         P(g.edges), plan.emu_blocks + k0 * 16, k1 - k0, x, 1.0, None, d,
                         plan.emu_rel + k0 * d * engine.LGCN_EMU_CANDS * 4,
                         plan.emu_meta + k0 * d * engine.LGCN_EMU_META_BYTES,
-                        plan.emu_stage + k0 * (d + 1) * engine.LGCN_EMU_BLOCK * 4, st) == 0
+                        plan.emu_stage + k0 * (d + 1) * engine.LGCN_EMU_BLOCK * 4, None, st) == 0
                 t["part0_blocks"] = timed(lambda: blocks(0, b0))
                 t["part1_blocks"] = timed(lambda: blocks(b0, b1))
                 t["blocks_all_walked"] = timed(lambda: blocks(0, b1))
@@ -90,7 +90,7 @@ def main():
                     assert lib.lgcn_emu_walk(P(g.edges), plan.emu_blocks,
                                              hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
                                              plan.emu_meta, plan.emu_stage, x, 1.0, None, P(y),
-                                             d, d, ctypes.byref(ep), sl, st) == 0
+                                             d, d, ctypes.byref(ep), sl, None, st) == 0
                 blocks(0, b1)
                 t["walk_row0"] = timed(lambda: walk(0, 1, slots[0]))
                 if r0 > 0:

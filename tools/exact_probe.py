@@ -142,7 +142,7 @@ def walk_timing(g, segs, d, thr, emu_min):
     y = torch.empty((g.n_rows, d), device=g.device)
     ep = engine._epilogue(engine.LGCN_EPI_STORE)
     assert lib.lgcn_emu_blocks(engine._ptr(g.edges), plan.emu_blocks, hp.n_emu_blocks, x, 1.0, None,
-                               d, plan.emu_rel, plan.emu_meta, plan.emu_stage, st) == 0
+                               d, plan.emu_rel, plan.emu_meta, plan.emu_stage, None, st) == 0
     has_modes = bool(os.environ.get("LGCN_LIB")) and hasattr(lib, "lgcn_emu_set_mode")
     has_stats = has_modes and hasattr(lib, "lgcn_emu_stats")
     if has_modes:
@@ -162,7 +162,7 @@ def walk_timing(g, segs, d, thr, emu_min):
             assert lib.lgcn_emu_walk(engine._ptr(g.edges), plan.emu_blocks,
                                      hp.emu_rows[lo:].data_ptr(), hi - lo, plan.emu_rel,
                                      plan.emu_meta, plan.emu_stage, x, 1.0, None, engine._ptr(y),
-                                     d, d, ctypes.byref(ep), engine.emu_slots()[0], st) == 0
+                                     d, d, ctypes.byref(ep), engine.emu_slots()[0], None, st) == 0
             b.record()
             torch.cuda.synchronize()
             print(f"  walk rows [{lo}, {hi}): {a.elapsed_time(b):.3f} ms", flush=True)

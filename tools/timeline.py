@@ -8,6 +8,7 @@ import argparse
 import csv
 import glob
 import os
+import re
 from collections import defaultdict
 
 
@@ -39,7 +40,8 @@ def bursts(rows, gap_ns=20_000_000):
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = re.sub(r"^void ", "", name)
+    name = re.sub(r"\(.*$", "", name.replace("(anonymous namespace)::", ""))
     return name if len(name) < 70 else name[:67] + "..."
 
 
