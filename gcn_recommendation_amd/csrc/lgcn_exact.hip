@@ -858,6 +858,9 @@ int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
 // reference's arithmetic, no emulation, no block pass. Edge records come in by LDS-DMA one
 // window further ahead, so the gather addresses are read from LDS, never waited on alone.
 // Ring: X windows w (folding), w+1 (in flight), w+2 (being issued); records w .. w+3.
+#ifndef LGCN_CHAIN_AHEAD32
+#define LGCN_CHAIN_AHEAD32 6  // X windows in flight per 32-column chain wave (build-time A/B)
+#endif
 template <int W>
 struct ChainCfg {
     static constexpr int LPR = W / 4;       // lanes per gathered row slice (16 B each)
@@ -866,7 +869,7 @@ struct ChainCfg {
     static constexpr int XWIN = 64 * W;     // floats per X window
     // X windows in flight while one is folded: as many as vmcnt (<= 63 outstanding) allows
     // with NI + 2 loads per window (W=64: 3 x 18, W=32: 6 x 10, W=16: 8 x 6)
-    static constexpr int AHEAD = W == 64 ? 3 : W == 32 ? 6 : 8;
+    static constexpr int AHEAD = W == 64 ? 3 : W == 32 ? LGCN_CHAIN_AHEAD32 : 8;
     static constexpr int NX = AHEAD + 1;    // X windows in the ring
     static constexpr int NR = 2 * AHEAD + 1;  // record windows in the ring
 };

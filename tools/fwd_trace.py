@@ -39,6 +39,23 @@ def main():
     runs = [("forward", lambda: engine.propagate_forward(g, segs, K)),
             ("backward", lambda: engine.propagate_backward(g, G, K)),
             ("backward_bpr", lambda: engine.propagate_backward(g, Gs, K))]
+    if os.environ.get("FWD_ONLY"):  # A/B timing: median of REPS forwards (and BPR backwards)
+        reps = int(os.environ.get("REPS", "10"))
+        for name, fn in (runs[0], runs[2]):
+            for _ in range(3):
+                fn()
+            ts = []
+            for _ in range(reps):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                fn()
+                b.record()
+                torch.cuda.synchronize()
+                ts.append(a.elapsed_time(b))
+            print(f"{name}: median {np.median(ts):.3f} ms min {min(ts):.3f} "
+                  f"[{os.environ.get('LGCN_LIB', 'product')} slots={os.environ.get('LGCN_EMU_SLOTS', '')}]",
+                  flush=True)
+        return
     for _, fn in runs:
         for _ in range(3):
             fn()
