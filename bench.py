@@ -466,7 +466,7 @@ def main():
         torch.cuda.synchronize()
         tr, engine.side_trace = engine.side_trace[0], None
         t0_ = tr[(1, 0)][0][1]
-        return {f"layer{k}_side{s}_lane{(k + s) % 2}":
+        return {f"layer{k}_side{s}_lane{(k + s + K) % 2}":
                 {nm: round(t0_.elapsed_time(ev), 3) for nm, ev in tr[(k, s)][1:]}
                 for (k, s) in sorted(tr)}
 
@@ -574,7 +574,7 @@ def main():
     if sided:
         result["phases_ms"] = {"forward": side_phases(lambda: step(mode=hub_mode)),
                                "note": "one forward's half-layers (layer k, side s on lane "
-                                       "(k+s)%2; side 0 = users(+brands), 1 = items): ms from "
+                                       "(k+s+K)%2; side 0 = users(+brands), 1 = items): ms from "
                                        "the first fork at which each part is done"}
 
     # BASELINE configs[3] on the same graph (d=256, K=4): the 1-GPU side of the 8-GPU target

@@ -1252,7 +1252,7 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
         // the item side first: its half-layer holds the longest walks (host submission order
         // only; the two sides of one layer are independent)
         for (int side = 1; side >= 0; --side) {
-            const Lane& L = lanes[(k + side) & 1];
+            const Lane& L = lanes[(k + side + K) & 1];
             // the mean of a side reads its layer K-1, computed on the other lane
             if (two && k == K && K >= 2)
                 if (int e = herr(hipStreamWaitEvent(L.main, sched->cross[side], 0))) return e;
@@ -1297,7 +1297,7 @@ int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edge
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
         for (int side = 1; side >= 0; --side)
             if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, h, xdiv, x_nz,
-                                   y, d, ep, sched, lanes[(k + side) & 1]))
+                                   y, d, ep, sched, lanes[(k + side + K) & 1]))
                 return e;
         h = dense_rows(y, n, d);
         xdiv = 1.f;

@@ -412,6 +412,39 @@ __device__ __forceinline__ uint32_t seq_reg(const float (&vv)[4], const float (&
     return (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(acc), L1);
 }
 
+// A whole block's chain (256 steps) over its (val, x) pairs in an LDS slot, S steps per lane:
+// lane l < 256/S holds steps S*l .. S*l+S-1 in registers and the value travels down those lanes
+// by DPP wave_shr:1 — 256/S - 1 lane transitions instead of seq_reg's 63 (a transition costs the
+// wait states around the DPP move on the dependent chain). The other lanes mirror the first
+// lanes' pairs and compute values nobody reads. Returns the bits of the value after step 255.
+#ifndef LGCN_SEQ_STEPS
+#define LGCN_SEQ_STEPS 16
+#endif
+template <int S>
+__device__ __forceinline__ uint32_t seq_block(const float* __restrict__ sv,
+                                              const float* __restrict__ sx, uint32_t a) {
+    constexpr int NL = LGCN_EMU_BLOCK / S;
+    static_assert(S % 4 == 0 && NL >= 1 && NL <= 64, "steps per lane");
+    const int l = threadIdx.x & (NL - 1);
+    const float4* v4 = reinterpret_cast<const float4*>(sv + S * l);
+    const float4* x4 = reinterpret_cast<const float4*>(sx + S * l);
+    float vv[S], xv[S];
+#pragma unroll
+    for (int q = 0; q < S / 4; ++q) {
+        const float4 v = v4[q], x = x4[q];
+        vv[4 * q] = v.x, vv[4 * q + 1] = v.y, vv[4 * q + 2] = v.z, vv[4 * q + 3] = v.w;
+        xv[4 * q] = x.x, xv[4 * q + 1] = x.y, xv[4 * q + 2] = x.z, xv[4 * q + 3] = x.w;
+    }
+    float acc = __uint_as_float(a);
+#pragma unroll
+    for (int L = 0; L < NL; ++L) {
+        if (L > 0) acc = dpp_wave_shr1(acc);
+#pragma unroll
+        for (int k = 0; k < S; ++k) acc = __builtin_fmaf(vv[k], xv[k], acc);
+    }
+    return (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(acc), NL - 1);
+}
+
 // The resolution of one block: the sequential chain a = fma(v_j, x_j, a), j < n, over the
 // block's (val, x) pairs in an LDS slot (sv, sx), read once into registers (lane l: steps
 // 4l..4l+3). With max_it = 0 (the default) it is the chain itself (seq_reg). Otherwise up to
@@ -427,6 +460,8 @@ __device__ __forceinline__ uint32_t resolve_block(const float* __restrict__ sv,
                                                   int max_it, unsigned long long* iters) {
     constexpr int kBurst = 16;
     const int lane = threadIdx.x;
+    // a whole block (every block of a row but possibly its last): LGCN_SEQ_STEPS per lane
+    if (max_it <= 0 && n == LGCN_EMU_BLOCK) return seq_block<LGCN_SEQ_STEPS>(sv, sx, a);
     const float4 v4 = *reinterpret_cast<const float4*>(sv + 4 * lane);
     const float4 x4 = *reinterpret_cast<const float4*>(sx + 4 * lane);
     const float vv[4] = {v4.x, v4.y, v4.z, v4.w};

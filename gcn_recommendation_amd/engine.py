@@ -836,16 +836,28 @@ def _check_emb(segments, d, device):
 _scheds = {}
 
 
-def _side_stream(device, i=0):
+def _side_stream(device, i=0, high=False):
     """Per-device side streams the emulated and chain rows run on beside the layer kernel
-    (lgcn_sched). Streams 0 and 4 carry the longest rows of lane 0 / lane 1 (a layer's critical
-    path): created at high priority (LGCN_EMU_PRIORITY=0: normal) so their waves are dispatched
-    first; stream 3 is lane 1's main stream."""
+    (lgcn_sched), one per (index, priority); high = created at high priority, so their waves are
+    dispatched first (LGCN_EMU_PRIORITY=0: every stream normal)."""
     sc = _scheds.setdefault(("streams", str(device)), {})
-    if i not in sc:
-        hi = i in (0, 4) and os.environ.get("LGCN_EMU_PRIORITY", "1") != "0"
-        sc[i] = torch.cuda.Stream(device, priority=-1 if hi else 0)
-    return sc[i]
+    high = high and os.environ.get("LGCN_EMU_PRIORITY", "1") != "0"
+    if (i, high) not in sc:
+        sc[(i, high)] = torch.cuda.Stream(device, priority=-1 if high else 0)
+    return sc[(i, high)]
+
+
+def _stream_priorities(n_aux):
+    """Which auxiliary streams run at high priority. One lane (n_aux <= 3): aux 0, the longest
+    rows' walks (a layer's critical path). Two lanes: all of lane 1 (aux 3 = its main stream and
+    aux 4..6) — it carries the chain of half-layers ending in layer K's items, the propagation's
+    critical path (lgcn_propagate_*_sides); LGCN_LANE_PRIORITY=part0 instead raises each lane's
+    part-0 stream (aux 0 and 4)."""
+    if n_aux <= 3:
+        return [i == 0 for i in range(n_aux)]
+    if os.environ.get("LGCN_LANE_PRIORITY", "lane1") == "part0":
+        return [i in (0, 4) for i in range(n_aux)]
+    return [i >= 3 for i in range(n_aux)]
 
 
 def hw_queues():
@@ -873,7 +885,8 @@ class Sched:
     def __init__(self, device, n_aux):
         lib = load_library()
         self.lib, self.device, self.n_aux = lib, device, n_aux
-        self.streams = [_side_stream(device, i) for i in range(n_aux)]
+        self.streams = [_side_stream(device, i, hi)
+                        for i, hi in enumerate(_stream_priorities(n_aux))]
         arr = (ctypes.c_void_p * n_aux)(*[st.cuda_stream for st in self.streams])
         h = ctypes.c_void_p()
         with torch.cuda.device(device):
@@ -910,7 +923,8 @@ def sched_for(device, n_aux=None):
     stream). n_aux: default n_aux_streams()."""
     if not emu_overlap_enabled():
         return None
-    key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled())
+    key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
+           os.environ.get("LGCN_LANE_PRIORITY", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
         if key[1] > 3:  # the one-lane schedule a capture falls back to, made outside any capture

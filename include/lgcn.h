@@ -470,8 +470,10 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
  * brands vs items, lgcn_csr_check_bipartite), so layer k of one side needs only layer k-1 of the
  * other. Every layer runs as two half-layers — slots [0, split) and [split, n) of a side-major
  * slot order (lgcn_csr_order_by_degree with side_lo < side_hi; split = its first slot of the
- * range side) — on two lanes: half-layer (k, side) on lane (k + side) % 2, each lane a chain of
- * half-layers that alternate sides. The longest rows' walks of one layer then overlap those of
+ * range side) — on two lanes: half-layer (k, side) on lane (k + side + K) % 2, each lane a chain
+ * of half-layers that alternate sides; lane 1 (aux_streams[3..]) carries the chain that ends in
+ * layer K's side-1 half-layer (the items': the longest rows), so its streams are the ones to
+ * create at high priority. The longest rows' walks of one layer then overlap those of
  * the next instead of queueing behind them. Same arguments and results (bitwise) as
  * lgcn_propagate_forward / _backward, except:
  *  - plans: 4 hub plans, plans[2 * side + j]: side's plan (built over its slot range, row ids
