@@ -1065,7 +1065,8 @@ int launch_chain(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                  float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, hipStream_t s) {
     // 128-B slices (one line per gathered row piece) for every d that is a multiple of 32: two
     // or more waves per row, each with twice the windows in flight of a 64-column wave
-    const int w = d % 32 == 0 ? 32 : 16;  // 16, 32 or a multiple of 64 (checked by the caller)
+    // (16- and 8-column slices: the d/P columns of a featsplit shard — d=64 at P=4, P=8)
+    const int w = d % 32 == 0 ? 32 : d % 16 == 0 ? 16 : 8;  // d % 8 == 0 (checked by the caller)
     const dim3 grid((uint32_t)n_rows, (uint32_t)((d + w - 1) / w));
     const bool seg1 = x.p0 == x.p1 && x.p1 == x.p2;
 #define LGCN_CH(W_, S_) \
@@ -1074,9 +1075,12 @@ int launch_chain(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     if (w == 32) {
         if (seg1) LGCN_CH(32, true);
         else LGCN_CH(32, false);
-    } else {
+    } else if (w == 16) {
         if (seg1) LGCN_CH(16, true);
         else LGCN_CH(16, false);
+    } else {
+        if (seg1) LGCN_CH(8, true);
+        else LGCN_CH(8, false);
     }
 #undef LGCN_CH
     return herr_x(hipGetLastError());
@@ -1333,7 +1337,7 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
 }
 
 
-int lgcn_chain_supported(int32_t d) { return d == 16 || d == 32 || (d > 0 && d % 64 == 0); }
+int lgcn_chain_supported(int32_t d) { return d > 0 && d <= 2048 && d % 8 == 0; }
 
 int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                     const lgcn_emu_row_t* rows, int32_t n_rows, lgcn_rows_t x, float x_div,

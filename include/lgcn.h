@@ -374,7 +374,8 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
  * wave per (row, column slice) folds acc = fma(val_j, X[col_j, c], acc) in stored order from +0
  * while the next windows of gathered X rows are in flight by LDS-DMA. rows / blocks: as for
  * lgcn_emu_walk (a row's edges are [blocks[first].beg, blocks[first + n - 1].end)). X rows and
- * segments 16-B aligned; d: lgcn_chain_supported(d) (16, 32 or a multiple of 64). x_nz is not
+ * segments 16-B aligned; d: lgcn_chain_supported(d) (a multiple of 8: slices of 32, 16 or 8
+ * columns — the last two for featsplit shards of d/P columns). x_nz is not
  * taken: dead rows of a row-sparse X are all zero, and folding them is exact. */
 int lgcn_chain_supported(int32_t d);
 int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,

@@ -101,17 +101,17 @@ def test_argument_validation_without_gpu(lib):
                              ctypes.byref(ep), 0, None, None) == -1
     assert lib.lgcn_emu_walk(None, None, None, 0, None, None, None, rows, 1.0, None, None, 64, 64,
                              ctypes.byref(ep), 64, None, None) == -1   # slots out of range
-    assert [lib.lgcn_chain_supported(d) for d in (8, 16, 24, 32, 64, 128, 192, 256)] == \
-        [0, 1, 0, 1, 1, 1, 1, 1]
+    assert [lib.lgcn_chain_supported(d) for d in (4, 8, 12, 16, 24, 32, 64, 100, 192, 256)] == \
+        [0, 1, 0, 1, 1, 1, 1, 0, 1, 1]
     assert lib.lgcn_chain_rows(None, None, None, 0, rows, 1.0, None, 64, 64, ctypes.byref(ep),
                                None) == 0     # nothing to do
-    assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 24, ctypes.byref(ep),
+    assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 12, ctypes.byref(ep),
                                None) == -1    # unsupported width
     assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8  # (+ padding, emu_live)
     # live-edge rows: the row mask and the scratch are required, widths as the chain kernel's
     assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, None, None, 64, 64,
                               ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # no x_nz
-    assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, ctypes.c_void_p(8), None, 64, 24,
+    assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, ctypes.c_void_p(8), None, 64, 12,
                               ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # width
     assert lib.lgcn_live_rows(None, None, 0, None, 0, rows, 1.0, ctypes.c_void_p(8), None, 64, 64,
                               ctypes.byref(ep), 0, 0, None, None) == 0   # nothing to do
