@@ -429,8 +429,9 @@ const char* lgcn_error_string(int code) {
 
 int32_t lgcn_chain_max_default(int64_t nnz) {
     // a chain row must stay short against a whole layer (C3: 56M nonzeros, ~3 ms per layer ->
-    // 55k edges; C2: 1.6M, ~0.07 ms -> the 2048 floor)
-    return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 1024, 2048), 65536);
+    // 55k edges); on a small graph the floor: a walk's fixed costs (block pass + walk ~0.4 ms per
+    // layer at C2) outweigh a 8k-edge chain (C2: 2048 -> 8192: forward 1.10 -> 0.94 ms)
+    return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 1024, 8192), 65536);
 }
 
 int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,

@@ -482,10 +482,12 @@ def test_plan_cache_reused_and_invalidated(gpu_device):
 
 
 @ORDERS
-def test_c2_scale_uniform_and_powerlaw(gpu_device, order):
+def test_c2_scale_uniform_and_powerlaw(gpu_device, monkeypatch, order):
     """BASELINE configs[1] shapes (50k x 50k, 1M interactions, d=64, K=3): the default (exact)
     plan bitwise forward and backward, on the one-operator and on the bipartite two-lane
-    schedule; the chunk plan within the north_star tolerance."""
+    schedule (forced: by default a graph this small keeps one operator); the chunk plan within
+    the north_star tolerance."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
     for gen in ("uniform", "powerlaw"):
         if gen == "uniform":
             u, i = graph.uniform_interactions(50_000, 50_000, 1_000_000, 1)

@@ -163,6 +163,6 @@ def test_c_planner_parts_and_scratch():
                                ctypes.byref(plan)) == -1
     assert lib.lgcn_plan_exact(rowptr.ctypes.data, None, deg.size, 128, 0, 0, rows.ctypes.data,
                                None, ctypes.byref(plan)) == -1
-    assert lib.lgcn_chain_max_default(1_600_000) == 2048
+    assert lib.lgcn_chain_max_default(1_600_000) == 8192
     assert lib.lgcn_chain_max_default(56_300_000) == 56_300_000 // 1024
     assert lib.lgcn_chain_max_default(10 ** 10) == 65536
