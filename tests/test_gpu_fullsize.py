@@ -89,6 +89,31 @@ def test_c3_books_d64_k3_exact(books, gpu_device):
     _check(books["rowptr"], books["c"], books["v"], segs, K, layers, final, sel, "C3")
 
 
+def test_c3_whole_table_bitwise_model_path(books, gpu_device):
+    """The whole C3 table, bitwise, through the model's own path: the drop-in LightGCN's
+    propagate_blocks (bipartite two-lane schedule, the items as sides) against the reference's
+    CPU forward itself (torch.sparse.mm ×3 + torch.mean(torch.stack), oracle.
+    reference_forward_torch, ~25 s on the box's host threads) — every one of the 14.7M rows."""
+    cfg = books["cfg"]
+    U, I, d, K = cfg["users"], cfg["items"], cfg["d"], cfg["K"]
+    gen = torch.Generator().manual_seed(42)
+    e0 = [bench.xavier(U, d, gen), bench.xavier(I, d, gen)]
+    with torch.no_grad():
+        out = engine.propagate_blocks(books["adj"], [t.to(gpu_device) for t in e0], K)
+    g = engine.graph_from_coo(books["adj"], sides=(U, U + I))
+    assert g.split is not None  # Â is bipartite across the items: the two-lane schedule ran
+    got = torch.cat([t.cpu() for t in out]).numpy()
+    del out
+    rowptr = books["rowptr"]
+    rows = np.repeat(np.arange(rowptr.size - 1, dtype=np.int64), np.diff(rowptr))
+    adj_cpu = torch.sparse_coo_tensor(torch.from_numpy(np.vstack((rows, books["c"]))),
+                                      torch.from_numpy(books["v"]), (books["n"], books["n"]))
+    del rows
+    want = oracle.reference_forward_torch(adj_cpu, torch.cat(e0, 0), K).numpy()
+    bad = np.nonzero(np.any(got.view(np.uint32) != want.view(np.uint32), axis=1))[0]
+    assert bad.size == 0, f"{bad.size} of {got.shape[0]} rows differ, first {bad[:5]}"
+
+
 def test_c4_books_d256_k4_exact(books, gpu_device):
     g = books["g"]
     n, d, K = books["n"], 256, 4
