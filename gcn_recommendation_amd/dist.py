@@ -234,8 +234,13 @@ class FeatSplitPlan:
     keeps the per-rank layers near the line-granular HBM floor. perm[s] = node id of slot s;
     results are bitwise those of the row-id layout (every row keeps its fp32 chain)."""
 
-    def __init__(self, rowptr, cols, vals, n, device):
-        g = engine.graph_from_host_csr(rowptr, cols, vals, n, device, order="degree")
+    def __init__(self, rowptr, cols, vals, n, device, sides=None):
+        """sides=(lo, hi): the item rows — a bipartite operator is stored side-major and each
+        rank's shard runs the two-lane schedule (engine.propagate_forward without per-layer
+        events), as the single-GPU path does."""
+        g = engine.graph_from_host_csr(rowptr, cols, vals, n, device, order="degree",
+                                       sides=sides)
+        self.sides = g.sides
         self.graph, self.perm = engine.relabel_slots(g)
         self.inv = torch.empty_like(self.perm)
         self.inv[self.perm] = torch.arange(n, dtype=self.perm.dtype, device=device)
@@ -268,7 +273,7 @@ class FeatSplitPlan:
         rt = cols[order]
         rpt = np.searchsorted(rt, np.arange(n + 1)).astype(np.int32)
         gt = engine.graph_from_host_csr(rpt, rows[order], vals[order], n, self.device,
-                                        order="degree")
+                                        order="degree", sides=self.sides)
         if not torch.equal(gt.row_ids.long(), self.perm):
             raise engine.LgcnError("featsplit: the transpose's slot order differs from Â's "
                                    "(non-symmetric pattern)")
@@ -492,18 +497,30 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
 
     if mode == "featsplit":
         rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
-        plan = FeatSplitPlan(rowptr, c, v, n, dev)
+        plan = FeatSplitPlan(rowptr, c, v, n, dev, sides=(U, U + I))
         x_slot, (c0, c1) = plan.shard(emb_host, world, rank)
         dl = c1 - c0
-        plan.graph.hubs(hub_thr)
+        sided = plan.graph.split is not None
+        if not sided:
+            plan.graph.hubs(hub_thr)
 
         def fn(timed):
+            if sided:  # the two-lane schedule has no layer boundary: one event pair per step
+                ev = [(torch.cuda.Event(enable_timing=True),
+                       torch.cuda.Event(enable_timing=True))] if timed else None
+                if ev:
+                    ev[0][0].record()
+                plan.forward(x_slot, K, hub_thr)
+                if ev:
+                    ev[0][1].record()
+                return ev
             ev = mk_events() if timed else None
             plan.forward(x_slot, K, hub_thr, layer_events=ev)
             return ev
         b_layer = nnz * (4 * dl + 8) + 4 * (n + 1) + 4 * n * dl
         comm = 0
-        extra = {"columns": [int(c0), int(c1)]}
+        extra = {"columns": [int(c0), int(c1)],
+                 "schedule": "bipartite two-lane" if sided else "one operator"}
     else:
         plan = RowPartPlan(r, c, v, n, world, rank, dev)
         segs = [t.to(dev) for t in emb_host]
@@ -517,6 +534,8 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
         extra = {"rows": [plan.r0, plan.r1], "nnz_local": plan.nnz_local}
 
     ms, lay = _timed(fn, args.steps, args.warmup, dev)
+    if lay.shape[1] == 1 and K > 1:  # sided featsplit: whole steps; a layer's share of one
+        lay = np.repeat(lay / K, K, axis=1)
     t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
                      dtype=torch.float64, device=dev)
     ms_max, kern_ms, all_ms = _max_over_ranks(t)

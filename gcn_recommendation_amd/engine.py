@@ -271,9 +271,11 @@ def pack_edges(cols, vals):
     return ((v << np.uint64(32)) | c).view(np.int64)
 
 
-def graph_from_host_csr(rowptr, cols, vals, n_cols, device, order=None):
+def graph_from_host_csr(rowptr, cols, vals, n_cols, device, order=None, sides=None):
     """Device CSR (possibly rectangular: a rank's row block with global columns) from host
-    arrays already in the engine's order. Forward-only: no transpose is attached."""
+    arrays already in the engine's order. Forward-only: no transpose is attached. sides=(lo, hi)
+    (square operators, degree order): side-major slots when the operator is bipartite across
+    [lo, hi) and large enough (sides_min_nnz), as graph_from_coo does."""
     rowptr = np.ascontiguousarray(rowptr, dtype=np.int32)
     n_rows = rowptr.size - 1
     nnz = int(rowptr[-1])
@@ -283,7 +285,12 @@ def graph_from_host_csr(rowptr, cols, vals, n_cols, device, order=None):
     g._rowptr_host = rowptr
     if row_order(order) == "degree":
         with torch.cuda.device(device):
-            g = order_by_degree(load_library(), g, _stream(device))
+            lib, st = load_library(), _stream(device)
+            mn = sides_min_nnz()
+            if sides is not None and (mn is None or nnz < mn or sides[0] >= sides[1] or
+                                      n_rows != n_cols or not is_bipartite(lib, g, sides, st)):
+                sides = None
+            g = order_by_degree(lib, g, st, sides)
     return g
 
 
@@ -702,6 +709,10 @@ def relabel_slots(g):
     o = Graph(g.n_rows, g.n_cols, g.rowptr, edges, g.nnz, dev)
     o._rowptr_host = g._rowptr_host
     o.symmetric = g.symmetric
+    if g.split is not None:  # side-major slots stay side-major: the sided schedule needs row ids
+        o.sides, o.split = g.sides, g.split
+        o.row_ids = torch.arange(g.n_rows, dtype=torch.int32, device=dev)
+        o._row_ids_host = np.arange(g.n_rows, dtype=np.int32)
     return o, perm
 
 

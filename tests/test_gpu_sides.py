@@ -124,3 +124,36 @@ def test_sides_refused_when_not_bipartite(gpu_device, monkeypatch):
     got = engine.propagate_forward(g, [torch.from_numpy(e0).to(gpu_device)], 2,
                                    **KW).cpu().numpy()
     assert np.array_equal(got, oracle.forward(r, c, v, e0, 2))
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_featsplit_shards_on_two_lanes(gpu_device, monkeypatch, brand_graph, P):
+    """dist.FeatSplitPlan with the item rows as sides (what bench.py --gpus P runs per rank): the
+    slot-space operator stays side-major, every rank's d/P columns propagate on the two-lane
+    schedule (d/P = 8 at P = 8: the chain kernel's 8-column slices), forward and backward
+    bitwise against the oracle per column block."""
+    from gcn_recommendation_amd import dist as D
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    r, c, v, n = brand_graph
+    d, K = 64, 3
+    rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
+    plan = D.FeatSplitPlan(rowptr, c, v, n, gpu_device, sides=(U, U + I))
+    assert plan.graph.split is not None and plan.sides == (U, U + I)
+    plan.attach_transpose(rowptr, c, v)
+    assert plan.graph.transpose.split is not None
+    rng = np.random.default_rng(31)
+    e0 = _e0(rng, "xavier", n, d)
+    segs = [torch.from_numpy(e0)]
+    want = oracle.forward(r, c, v, e0, K)
+    G = _e0(rng, "xavier", n, d)
+    want_g = oracle.backward(r, c, v, G, K)
+    cols, cols_b = [], []
+    for p in range(P):
+        x, (c0, c1) = plan.shard(segs, P, p)
+        assert c1 - c0 == d // P
+        cols.append(plan.unshard(plan.forward(x, K, 128, hub_mode="exact")).cpu().numpy())
+        gs = torch.from_numpy(np.ascontiguousarray(G[:, c0:c1])).to(gpu_device)[plan.perm]
+        cols_b.append(plan.unshard(plan.backward(gs.contiguous(), K, 128, sparse="off"))
+                      .cpu().numpy())
+    assert np.array_equal(np.concatenate(cols, 1), want)
+    assert np.array_equal(np.concatenate(cols_b, 1), want_g)
