@@ -385,8 +385,14 @@ def main():
                "bitwise_equal": bool(torch.equal(adj_dev._indices(), adj._indices()) and torch.equal(
                    adj_dev._values().view(torch.int32), adj._values().view(torch.int32)))}
     del adj_dev, inter, u_, i_
-    log(f"[bench] CSR plan {prep_s:.2f}s; hubs: {hp.n_rows} rows / {hp.n_items} chunks "
-        f"(threshold {hub_thr}); max degree {int(g.degrees().max())}")
+    if hp.mode == "exact":
+        log(f"[bench] CSR plan {prep_s:.2f}s; exact plan: {hp.n_emu_rows} rows above the "
+            f"threshold {hub_thr} ({hp.n_emu_blocks} emulation blocks; the shorter ones run as "
+            f"chains); max degree {int(g.degrees().max())}; "
+            f"schedule {'two lanes' if sided else 'one operator'}")
+    else:
+        log(f"[bench] CSR plan {prep_s:.2f}s; hubs: {hp.n_rows} rows / {hp.n_items} chunks "
+            f"(threshold {hub_thr}); max degree {int(g.degrees().max())}")
 
     if fusion:  # LightGCN_Fusion forward: [user | leaky_relu(Linear([id | content])) | brand]
         content = torch.from_numpy(np.random.default_rng(5).standard_normal(
