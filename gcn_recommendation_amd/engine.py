@@ -27,7 +27,7 @@ TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3,
 TUNE_EMU_RESOLVE = 5
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
-SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
+SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST = 7, 8, 9
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
@@ -908,6 +908,10 @@ class Sched:
         self.set(SCHED_SLOTS0, slots[0])
         self.set(SCHED_SLOTS1, slots[min(1, len(slots) - 1)])
         self.set(SCHED_CHAIN, 1 if chain_enabled() else 0)
+        # LGCN_BLOCKS_FIRST=1 (A/B with an LGCN_LIB build that has the knob): each
+        # layer kernel waits for its part 0 block pass
+        if os.environ.get("LGCN_BLOCKS_FIRST", "0") == "1":
+            self.set(SCHED_BLOCKS_FIRST, 1)
 
     def set(self, knob, value):
         _check(self.lib.lgcn_sched_set(self.handle, knob, int(value)), "lgcn_sched_set")
@@ -936,7 +940,7 @@ def sched_for(device, n_aux=None):
     if not emu_overlap_enabled():
         return None
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_LANE_PRIORITY", ""))
+           os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_BLOCKS_FIRST", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
         if key[1] > 3:  # the one-lane schedule a capture falls back to, made outside any capture
