@@ -800,6 +800,10 @@ struct lgcn_sched {
     hipEvent_t lane_fork, lane_join, cross[2];
     hipEvent_t* trace_sides;  // optional [16 K] (LGCN_SCHED_TRACE_SIDES)
     hipEvent_t* timing_sides; // optional [4 K] (LGCN_SCHED_TIMING_SIDES)
+    // LGCN_SCHED_BLOCKS_FIRST: the layer kernel waits for part 0's block pass (blocks_done), so
+    // the longest rows' walk starts before the layer kernel floods the chip
+    int blocks_first;
+    hipEvent_t blocks_done;
 };
 
 namespace {
@@ -958,6 +962,10 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
             if (i < 2)
                 if (int e = mark(1 + i, aux_of(i))) return e;
         }
+    if (sc->blocks_first && sc->blocks_done && parts[0].b1 > parts[0].b0) {
+        if (int e = herr(hipEventRecord(sc->blocks_done, aux_of(0)))) return e;
+        if (int e = herr(hipStreamWaitEvent(s, sc->blocks_done, 0))) return e;
+    }
     if (int e = layer_kernel(s)) return e;
     if (int e = mark(3, s)) return e;
     if (chains) {
@@ -1092,6 +1100,7 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
     auto mk = [](hipEvent_t* ev) { return herr(hipEventCreateWithFlags(ev, hipEventDisableTiming)); };
     int e = mk(&sc->fork);
     for (int i = 0; i < n0 && !e; ++i) e = mk(&sc->join[i]);
+    if (!e) e = mk(&sc->blocks_done);
     if (!e && n_aux >= 4) {
         sc->lane1_main = reinterpret_cast<hipStream_t>(aux_streams[3]);
         sc->lane1 = new (std::nothrow) lgcn_sched();
@@ -1105,6 +1114,7 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
                 l1->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[4 + i]);
             e = mk(&l1->fork);
             for (int i = 0; i < l1->n_aux && !e; ++i) e = mk(&l1->join[i]);
+            if (!e) e = mk(&l1->blocks_done);
             if (!e) e = mk(&sc->lane_fork);
             if (!e) e = mk(&sc->lane_join);
             for (int i = 0; i < 2 && !e; ++i) e = mk(&sc->cross[i]);
@@ -1121,6 +1131,7 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
 int lgcn_sched_destroy(lgcn_sched_t* sc) {
     if (!sc) return 0;
     if (sc->fork) (void)hipEventDestroy(sc->fork);
+    if (sc->blocks_done) (void)hipEventDestroy(sc->blocks_done);
     for (int i = 0; i < 3; ++i)
         if (sc->join[i]) (void)hipEventDestroy(sc->join[i]);
     hipEvent_t* own[] = {&sc->lane_fork, &sc->lane_join, &sc->cross[0], &sc->cross[1]};
@@ -1155,6 +1166,10 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
             return 0;
         case LGCN_SCHED_TRACE_SIDES:
             sc->trace_sides = reinterpret_cast<hipEvent_t*>(value);
+            return 0;
+        case LGCN_SCHED_BLOCKS_FIRST:
+            sc->blocks_first = value != 0;
+            if (sc->lane1) sc->lane1->blocks_first = value != 0;
             return 0;
         case LGCN_SCHED_TIMING_SIDES:
             sc->timing_sides = reinterpret_cast<hipEvent_t*>(value);

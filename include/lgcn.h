@@ -435,6 +435,10 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
 #define LGCN_SCHED_TIMING_SIDES  8  /* hipEvent_t[4 * K] (or 0): recorded on its lane's stream right
                                        before / after the layer kernel of half-layer (k, side), at
                                        [((k - 1) * 2 + side) * 2] and [... + 1] (timing) */
+#define LGCN_SCHED_BLOCKS_FIRST  9  /* 1: a layer kernel waits for its part 0 block pass (the
+                                       longest rows' walk then starts before the layer kernel
+                                       fills the chip; engine.py sets it); 0 (the C default):
+                                       they start together */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +
