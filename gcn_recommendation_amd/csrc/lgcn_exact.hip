@@ -40,6 +40,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "lgcn.h"
 
 namespace lgcn_detail {
@@ -122,6 +124,14 @@ __device__ __forceinline__ int lsb_exp_prod(float v, float x) {
 // ---------------------------------------------------------------------------------------------
 // block pass: one wave per (block, 64-column slice); lane = column
 // ---------------------------------------------------------------------------------------------
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+// timing experiments only (tools/exact_layer_probe.py --blk-modes): bit 1 = no stage writes,
+// 2 = no candidate chains, 4 = no lowest-set-bit tracking (the tables are then wrong)
+__device__ int g_blk_mode;
+#define LGCN_BLK_OFF(b) ((blk_mode & (b)) != 0)
+#else
+#define LGCN_BLK_OFF(b) false
+#endif
 template <int XD>
 __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict__ edges,
                                                    const lgcn_emu_block_t* __restrict__ blocks,
@@ -138,6 +148,9 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     const lgcn_emu_block_t blk = blocks[blockIdx.x];
     // a row the live-edge chains run (lgcn_live_rows flags it) needs no block pass
     if (live && live[blk.row].n_blocks) return;
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+    const int blk_mode = __builtin_amdgcn_readfirstlane(g_blk_mode);
+#endif
     // T: the sequential fma chain of the block from +0. It is the true chain for block 0; for
     // every block it tracks the exact running sum S of the products to within 1/2 ulp(|T|) per
     // step, which bounds every trajectory of the block (meta lo0/hi0)
@@ -167,7 +180,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     float* sv = stage && blockIdx.y == 0
                     ? stage + ((int64_t)blockIdx.x * (d + 1) + d) * LGCN_EMU_BLOCK : nullptr;
     auto stage_sub = [&](const float (&xv)[SW], int step0) {
-        if (!st || !act) return;
+        if (!st || !act || LGCN_BLK_OFF(1)) return;
 #pragma unroll
         for (int q = 0; q < SW / 4; ++q)
             *reinterpret_cast<float4*>(st + step0 + 4 * q) =
@@ -203,9 +216,9 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             T = __builtin_fmaf(vv[t], xv[t], T);
             tlo = fminf(tlo, T);
             thi = fmaxf(thi, T);
-            maxlsb = max(maxlsb, lsb_exp_prod(vv[t], xv[t]));
+            if (!LGCN_BLK_OFF(4)) maxlsb = max(maxlsb, lsb_exp_prod(vv[t], xv[t]));
         }
-        if (init) {
+        if (init && !LGCN_BLK_OFF(2)) {
 #pragma unroll
             for (int t = 0; t < SW; ++t) {
 #pragma unroll
@@ -632,7 +645,8 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // Chunk ch's blocks predicted to need a resolve, from the approximate start bits pa, in ONE
     // pass: block i's start is taken as pa + the chains from +0 (meta r0) of the blocks before
     // it — the true contributions to within their rounding — and every lane tests its own block
-    // from its own start with widened bounds. The lowest NS predicted blocks are recorded.
+    // from its own start with widened bounds. All predicted blocks are recorded (the first NS
+    // are fetched ahead of the chunk, the rest refill slots as the walk passes them).
     // Returns the approximate end value.
     auto predict = [&](int ch, int buf, const int4& m, uint32_t pa,
                        unsigned long long& pred) -> uint32_t {
@@ -655,15 +669,14 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         const int alo = neg ? -hi : lo, ahi = neg ? -lo : hi;
         const int mg = ((hi - lo) >> 3) + 256;
         const bool ok = ident || (inw && M + alo >= kLB + mg && M + ahi <= kHB - mg);
-        unsigned long long bad = __ballot(act && !ok);
-        // keep the NS lowest
-        unsigned long long keep = 0;
-        for (int i = 0; i < NS && bad; ++i) {
-            const unsigned long long lowbit = bad & (~bad + 1ull);
-            keep |= lowbit;
-            bad ^= lowbit;
+        pred = __ballot(act && !ok);
+#ifdef LGCN_WALK_NO_REFILL  // build-time A/B: the first NS only, the rest fetched on demand
+        {
+            unsigned long long keep = 0, m = pred;
+            for (int i = 0; i < NS && m; ++i, m &= m - 1) keep |= m & (~m + 1ull);
+            pred = keep;
         }
-        pred = keep;
+#endif
         const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
         return (uint32_t)__builtin_amdgcn_readfirstlane(
             (int)__float_as_uint(__uint_as_float(pa) + tot));
@@ -672,35 +685,54 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         dma16(stage + (bi * (d + 1) + d) * B + 4 * lane, lds_byte(slot_v(slot)));
         dma16(stage + (bi * (d + 1) + c) * B + 4 * lane, lds_byte(slot_x(slot)));
     };
-    auto issue_slots = [&](int ch, unsigned long long pred, int set) {
-        int s = 0;
-        for (unsigned long long m = pred; m; m &= m - 1, ++s)
+    // the first NS predicted blocks of chunk ch into slot set `set`; returns the predicted
+    // blocks left for refills (nvm: this wave's vector-memory operations issued so far)
+    auto issue_slots = [&](int ch, unsigned long long pred, int set,
+                           int& nvm) -> unsigned long long {
+        unsigned long long m = pred;
+        for (int s = 0; s < NS && m; ++s, m &= m - 1) {
             fetch(fb + 1 + (int64_t)ch * CH + __builtin_ctzll(m), set * NS + s);
+            nvm += 2;
+        }
+        return m;
     };
     if (nch > 0) {
         Tab tn;
         int4 mc, mn = make_int4(0, 0, 0, 0);
+        // vmcnt bookkeeping: nvm counts this wave's vector-memory operations (5 per table load,
+        // 2 per block fetch); an operation stamped s has landed once at most nvm - s younger
+        // ones are outstanding (they complete in issue order)
+        int nvm = 0;
         load_tab(0, tn);
+        nvm += 5;
         stage_tab(tn, 0);
         mc = tn.m;
         unsigned long long pred_c = 0, pred_n = 0;
         uint32_t start_c = ab;                     // assumed start of chunk ch's prediction
         uint32_t end_c = predict(0, 0, mc, ab, pred_c);  // and its predicted end
         if (!staged) pred_c = 0;
-        issue_slots(0, pred_c, 0);
+        // predicted blocks of chunk ch not fetched yet, how many are issued, and the stamp of
+        // its first NS fetches; lane k of `stamp`: nvm after the fetch of predicted block #k
+        unsigned long long rem_c = issue_slots(0, pred_c, 0, nvm), rem_n = 0;
+        int iss_c = min(__builtin_popcountll(pred_c), NS), iss_n = 0;
+        int stamp_c = nvm, stamp_n = 0;
+        int stamp = 0;
         if (nch > 1) {
             load_tab(1, tn);
+            nvm += 5;
             stage_tab(tn, 1);
             mn = tn.m;
         }
-        if (nch > 2) load_tab(2, tn);  // in flight during chunk 0
+        if (nch > 2) {  // in flight during chunk 0
+            load_tab(2, tn);
+            nvm += 5;
+        }
         PH_MARK(0);
         for (int ch = 0; ch < nch; ++ch) {
             const int buf = ch & 1;
             const int nb = chunk_nb(ch);
             // prediction of chunk ch + 1 (its start: chunk ch's predicted end, moved by the
-            // error of chunk ch's assumed start) and its slot fetches, in flight during ch
-            int after = ch + 2 < nch ? 5 : 0;  // loads issued after chunk ch's slots: table ch+2
+            // error of chunk ch's assumed start) and its first slot fetches, in flight during ch
             uint32_t start_n = 0, end_n = 0;
             if (ch + 1 < nch) {
                 start_n = __float_as_uint(__uint_as_float(end_c) +
@@ -708,13 +740,14 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                 start_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)start_n);
                 end_n = predict(ch + 1, buf ^ 1, mn, start_n, pred_n);
                 if (!staged) pred_n = 0;
-                issue_slots(ch + 1, pred_n, buf ^ 1);
-                after += 2 * __builtin_popcountll(pred_n);
+                rem_n = issue_slots(ch + 1, pred_n, buf ^ 1, nvm);
+                iss_n = min(__builtin_popcountll(pred_n), NS);
+                stamp_n = nvm;
             }
             PH_MARK(1);
             PH_COUNT(8, 1);
             PH_COUNT(9, __builtin_popcountll(pred_c));
-            wait_vm_upto(after);  // chunk ch's slots have landed
+            wait_vm_upto(nvm - stamp_c);  // chunk ch's first slots have landed
             PH_MARK(2);
             int from = 0;
             while (true) {
@@ -730,6 +763,16 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                 n_fast += f - from;
 #endif
                 if (f >= nb) break;
+                // refills: the predicted blocks before f are done, their slots take the next
+                // predicted ones (at most NS ahead of f, so f's own slot is kept)
+                const int done = __builtin_popcountll(pred_c & ((1ull << f) - 1ull));
+                while (rem_c && iss_c < done + NS) {
+                    fetch(fb + 1 + (int64_t)ch * CH + __builtin_ctzll(rem_c), buf * NS + iss_c % NS);
+                    nvm += 2;
+                    stamp = lane == iss_c ? nvm : stamp;
+                    rem_c &= rem_c - 1;
+                    ++iss_c;
+                }
                 const int kb = 1 + ch * CH + f;  // block index in the row
                 const int32_t bbeg = row_beg + kb * B;
                 const int n = min(bbeg + B, row_end) - bbeg;
@@ -739,13 +782,19 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
 #endif
                 int sl;
                 if ((pred_c >> f) & 1ull) {
-                    sl = buf * NS + __builtin_popcountll(pred_c & ((1ull << f) - 1ull));
+                    sl = buf * NS + done % NS;
+                    if (done >= NS) {  // a refill: wait for its own fetch only
+                        wait_vm_upto(nvm - __builtin_amdgcn_readlane(stamp, done));
+                        PH_MARK(5);
+                    }
                 } else {  // not predicted: fetched now into the spare slot
                     sl = spare;
                     EMU_STAT(3, 1);
                     PH_COUNT(11, 1);
                     if (staged) {
                         fetch(fb + kb, sl);
+                        nvm += 2;
+                        // the youngest operation: everything older lands before it anyway
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     } else {
                         // no stage: the block's edge records and X elements, gathered
@@ -786,9 +835,15 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
             } else {
                 mc = mn;
             }
-            if (ch + 3 < nch) load_tab(ch + 3, tn);
+            if (ch + 3 < nch) {
+                load_tab(ch + 3, tn);
+                nvm += 5;
+            }
             PH_MARK(0);
             pred_c = pred_n;
+            rem_c = rem_n;
+            iss_c = iss_n;
+            stamp_c = stamp_n;
             start_c = start_n;
             end_c = end_n;
         }
@@ -851,11 +906,20 @@ int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                 const lgcn_emu_row_t* live, hipStream_t s) {
     const dim3 grid((uint32_t)n_rows, (uint32_t)d);
     const size_t lds = (size_t)(2 * slots + 1) * 2 * LGCN_EMU_BLOCK * sizeof(float);
-    if (lds > 56 * 1024) {  // beyond the default dynamic-LDS limit: raise it once per kernel
-        static const hipError_t once = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&k_emu_walk<MODE, XD>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
-        if (once != hipSuccess) return (int)once;
+    if (lds > 56 * 1024) {
+        // beyond the default dynamic-LDS limit: raise it once per kernel and DEVICE (the
+        // attribute applies to the device current at the call)
+        static std::atomic<uint64_t> raised{0};
+        int dev = 0;
+        if (hipError_t e = hipGetDevice(&dev)) return (int)e;
+        const uint64_t bit = dev < 64 ? (1ull << dev) : 0;
+        if (!bit || !(raised.load(std::memory_order_relaxed) & bit)) {
+            const hipError_t e = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&k_emu_walk<MODE, XD>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
+            if (e != hipSuccess) return (int)e;
+            raised.fetch_or(bit, std::memory_order_relaxed);
+        }
     }
     hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, ktab,
                        meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots, lgcn_detail::g_emu_resolve,
@@ -1240,6 +1304,9 @@ extern "C" {
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
 int lgcn_emu_set_mode(int mode) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_emu_mode), &mode, sizeof(int)) == hipSuccess ? 0 : -1;
+}
+int lgcn_emu_set_blk_mode(int mode) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_blk_mode), &mode, sizeof(int)) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -930,7 +930,8 @@ def _capture_aux(device):
     hipStreamEndCapture on this ROCm (segfault, tests/test_gpu_sides.py), so a captured sided
     propagation runs its half-layers in order on one lane — same kernels, same bits."""
     if torch.cuda.is_current_stream_capturing():
-        return min(3, n_aux_streams())
+        cap = os.environ.get("LGCN_CAPTURE_AUX", "")
+        return min(int(cap) if cap else 3, n_aux_streams())
     return None
 
 

@@ -362,8 +362,11 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
  * flagged n_blocks != 0 are skipped: lgcn_live_rows wrote them). Needs lgcn_emu_blocks' rel / meta (and stage, if it wrote
  * one; NULL = blocks to resolve gather X) of the same X. slots: LDS slots per 64-block chunk
  * for the blocks predicted to need an in-block resolve, 1..LGCN_EMU_MAX_WALK_SLOTS (0 = the
- * default, 12): 4 KB of LDS per wave each (two chunks in flight), so a walk over short rows
- * runs more waves per CU with fewer slots, and the longest rows (few waves) take many. */
+ * library default, 12; the Python binding and INTEGRATION.md's C recipe pass 20 for part 0 and
+ * 8 for part 1): 4 KB of LDS per wave each (two chunks in flight), so a walk over short rows
+ * runs more waves per CU with fewer slots, and the longest rows (few waves) take many. A chunk
+ * with more predicted blocks than slots refills a slot as soon as the walk has passed the block
+ * it held. */
 int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,

@@ -11,6 +11,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from gcn_recommendation_amd import engine  # noqa: E402
 import test_gpu_sides as T  # noqa: E402
 
+if os.environ.get("LGCN_SEGV_TRACE"):  # native backtrace of a host crash (tools/segv_trace.c)
+    import ctypes
+    ctypes.CDLL(os.path.join(ROOT, "tools", "libsegv_trace.so"))
 os.environ["LGCN_SIDES_MIN_NNZ"] = "0"
 os.environ["LGCN_AUX_STREAMS"] = sys.argv[1]
 dev = torch.device("cuda:0")

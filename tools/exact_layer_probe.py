@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--emu-min", default="0")
     ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--blk-modes", default="",
+                    help="with a LGCN_EMU_MODES/STATS build (LGCN_LIB): block-pass timing with "
+                         "parts switched off, e.g. 1,2,4,7 (1 stage, 2 candidates, 4 lsb)")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     dev = torch.device("cuda:0")
@@ -83,6 +86,11 @@ def main():
                         plan.emu_stage + k0 * (d + 1) * engine.LGCN_EMU_BLOCK * 4, None, st) == 0
                 t["part0_blocks"] = timed(lambda: blocks(0, b0))
                 t["part1_blocks"] = timed(lambda: blocks(b0, b1))
+                for m in [int(k) for k in a.blk_modes.split(",") if k.strip()]:
+                    lib.lgcn_emu_set_blk_mode(m)
+                    t[f"part0_blocks_off{m}"] = timed(lambda: blocks(0, b0))
+                    t[f"part1_blocks_off{m}"] = timed(lambda: blocks(b0, b1))
+                    lib.lgcn_emu_set_blk_mode(0)
                 t["blocks_all_walked"] = timed(lambda: blocks(0, b1))
                 slots = engine.emu_slots()
 
