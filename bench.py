@@ -17,12 +17,13 @@ import os
 import sys
 import time
 
-# The bipartite two-lane schedule runs 8 streams (lgcn_sched_create: the caller's + 7); every
-# stream wants a hardware queue of its own, and HIP reads this once, when the process first
-# touches the GPU (its default, 4, makes the lanes share queues: same bits, less overlap).
-# LGCN_HW_QUEUES=keep leaves the environment's value alone.
-if os.environ.get("LGCN_HW_QUEUES", "") != "keep":
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LGCN_HW_QUEUES", "") or "8"
+# The bipartite two-lane schedule runs 8 streams (lgcn_sched_create: the caller's + 7). HIP keeps
+# GPU_MAX_HW_QUEUES hardware queues (default 4) per stream priority, and the second lane's four
+# streams are high priority: every stream gets a queue under the default, which is what
+# main.py runs with (round 4: 17.08 ms at 4 queues vs 17.17 ms at 8). The environment is left
+# alone; LGCN_HW_QUEUES=N sets GPU_MAX_HW_QUEUES for an A/B.
+if os.environ.get("LGCN_HW_QUEUES", ""):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LGCN_HW_QUEUES"]
 
 import numpy as np
 import torch
@@ -569,7 +570,7 @@ def main():
                    "emu_min_degree": engine.emu_min_degree_from_env(),
                    "schedule": ("bipartite two-lane (lgcn_propagate_forward_sides), "
                                 f"{engine.n_aux_streams()} aux streams, GPU_MAX_HW_QUEUES="
-                                f"{engine.hw_queues()}") if sided else "one operator",
+                                f"{os.environ.get('GPU_MAX_HW_QUEUES', 'unset (HIP default 4)')}") if sided else "one operator",
                    "parallelism": "single"},
         "roofline": roof,
         "wall_s_timed": round(wall, 3), "prep_s": round(prep_s, 2),

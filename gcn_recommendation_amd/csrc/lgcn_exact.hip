@@ -107,13 +107,18 @@ __device__ __forceinline__ float load_elem(const lgcn_rows_t& x, const uint32_t*
     else return v;
 }
 
-// exponent of the lowest set bit of a finite nonzero float (subnormals included)
+// exponent of the lowest set bit of a finite nonzero float (subnormals included), branch-free:
+// the lowest set bit of the mantissa with the implicit bit 23 set (the exponent bits above it do
+// not matter; a subnormal's bits lie below it). A zero gives -126, below any nonzero float's.
 __device__ __forceinline__ int lsb_exp(float f) {
     const uint32_t b = __float_as_uint(f);
     const int E = (int)((b >> 23) & 255u);
-    const uint32_t M = b & 0x7fffffu;
-    if (E == 0) return -149 + __builtin_ctz(M);
-    return E - 150 + __builtin_ctz(M | 0x800000u);
+    return __builtin_ctz(b | 0x800000u) + max(E, 1) - 150;
+}
+
+// lsb_exp, and -100000 for +-0: the sum of two of them is < -50000 iff the product is zero
+__device__ __forceinline__ int lsb_exp_z(float f) {
+    return (__float_as_uint(f) << 1) ? lsb_exp(f) : -100000;
 }
 
 // lowest-set-bit exponent of the exact product v * x (-100000: the product is zero)
@@ -141,7 +146,12 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                                                    int4* __restrict__ meta,
                                                    float* __restrict__ stage,
                                                    const lgcn_emu_row_t* __restrict__ live) {
-    constexpr int SW = 16;  // steps gathered per sub-window (all in flight at once)
+    // steps gathered per sub-window (all in flight at once), two sub-windows in flight
+#ifndef LGCN_BLK_SW
+#define LGCN_BLK_SW 16
+#endif
+    constexpr int SW = LGCN_BLK_SW;
+    static_assert(SW == 8 || SW == 16, "sub-window");
     const int lane = threadIdx.x;
     const int c = blockIdx.y * 64 + lane;
     const bool act = c < d;
@@ -175,16 +185,35 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
         }
     };
     // this (block, column)'s elements, in step order (the walk resolves a block from here)
-    // stage layout [block][d + 1][BLOCK]: column c's X elements, then (column d) the edge values
-    float* st = stage ? stage + ((int64_t)blockIdx.x * (d + 1) + cc) * LGCN_EMU_BLOCK : nullptr;
+    // stage layout [block][d + 1][BLOCK]: column c's X elements, then (column d) the edge values.
+    // Written through an LDS tile of 32 steps x 64 columns: each flush stores 8 whole 128-B
+    // column runs per instruction. (A lane storing its own column's 16-B pieces at a 1-KB
+    // stride scattered 64 half-written lines over L2 per instruction: ~60% of the pass's time.)
+    constexpr int TP = 36;  // tile pitch in floats: 32 steps + 4 (ds_write_b128 conflict-free)
+    __shared__ __attribute__((aligned(16))) float s_tile[64 * TP];
+    float* const st0 = stage ? stage + (int64_t)blockIdx.x * (d + 1) * LGCN_EMU_BLOCK : nullptr;
     float* sv = stage && blockIdx.y == 0
                     ? stage + ((int64_t)blockIdx.x * (d + 1) + d) * LGCN_EMU_BLOCK : nullptr;
-    auto stage_sub = [&](const float (&xv)[SW], int step0) {
-        if (!st || !act || LGCN_BLK_OFF(1)) return;
+    const bool staging = st0 && !LGCN_BLK_OFF(1);
+    auto stage_sub = [&](const float (&xv)[SW], int part) {  // SW steps into the tile
+        if (!staging) return;
+        float* tp = s_tile + lane * TP + SW * part;
 #pragma unroll
         for (int q = 0; q < SW / 4; ++q)
-            *reinterpret_cast<float4*>(st + step0 + 4 * q) =
+            *reinterpret_cast<float4*>(tp + 4 * q) =
                 make_float4(xv[4 * q], xv[4 * q + 1], xv[4 * q + 2], xv[4 * q + 3]);
+    };
+    auto stage_flush = [&](int step0) {  // the tile's 32 steps -> stage, 8 columns a store
+        if (!staging) return;
+        const int sub = lane >> 3, q = lane & 7;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int col = 8 * i + sub;
+            const float4 v = *reinterpret_cast<const float4*>(s_tile + col * TP + 4 * q);
+            const int cg = blockIdx.y * 64 + col;
+            if (cg < d)
+                *reinterpret_cast<float4*>(st0 + (int64_t)cg * LGCN_EMU_BLOCK + step0 + 4 * q) = v;
+        }
     };
     // one sub-window: steps past the block end read as (0, 0), and fma(0, 0, c) == c for every
     // chain value (a chain is never -0), so the unrolled steps need no guard
@@ -216,7 +245,8 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             T = __builtin_fmaf(vv[t], xv[t], T);
             tlo = fminf(tlo, T);
             thi = fmaxf(thi, T);
-            if (!LGCN_BLK_OFF(4)) maxlsb = max(maxlsb, lsb_exp_prod(vv[t], xv[t]));
+            // a product's lowest set bit: lsb(v) (scalar) + lsb(x); -100000 when v or x is a zero
+            if (!LGCN_BLK_OFF(4)) maxlsb = max(maxlsb, lsb_exp_z(vv[t]) + lsb_exp_z(xv[t]));
         }
         if (init && !LGCN_BLK_OFF(2)) {
 #pragma unroll
@@ -232,20 +262,19 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
         const int2 nrec = load_rec(j0 + 64);  // next window's records, in flight meanwhile
         if (sv) sv[j0 - blk.beg + lane] = __int_as_float(rec.y);  // (0 past the block end)
         float xa[SW], va[SW], xb[SW], vb[SW];
-        // the loads of sub-window k + 1 are issued before sub-window k is computed
         const int w0 = j0 - blk.beg;
+        // the loads of sub-window k + 1 are issued before sub-window k is computed
         load_sub(rec, 0, n, xa, va);
-        load_sub(rec, 16, n, xb, vb);
-        run_sub(xa, va);
-        stage_sub(xa, w0);
-        load_sub(rec, 32, n, xa, va);
-        run_sub(xb, vb);
-        stage_sub(xb, w0 + 16);
-        load_sub(rec, 48, n, xb, vb);
-        run_sub(xa, va);
-        stage_sub(xa, w0 + 32);
-        run_sub(xb, vb);
-        stage_sub(xb, w0 + 48);
+#pragma unroll
+        for (int k = 0; k < 64 / SW; k += 2) {
+            load_sub(rec, (k + 1) * SW, n, xb, vb);
+            run_sub(xa, va);
+            stage_sub(xa, k % (32 / SW));
+            if (k + 2 < 64 / SW) load_sub(rec, (k + 2) * SW, n, xa, va);
+            run_sub(xb, vb);
+            stage_sub(xb, (k + 1) % (32 / SW));
+            if ((k + 2) % (32 / SW) == 0) stage_flush(w0 + (k + 2 - 32 / SW) * SW);
+        }
         rec = nrec;
     }
     if (!act) return;
@@ -279,7 +308,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                         maxlsb < eb - 24;
         vm |= ok ? (1u << k) : 0u;
     }
-    const bool ident = maxlsb == -100000;
+    const bool ident = maxlsb < -50000;
     const int pk = ident ? (kIdentEb & 0xffff) : (int)(((uint32_t)ebase & 0xffffu) | (vm << 16));
     meta[rc] = make_int4(lo0, hi0, pk, __float_as_int(T));
     int4* kp = ktab + rc * 4;

@@ -881,12 +881,15 @@ def hw_queues():
 
 
 def n_aux_streams():
-    """Auxiliary streams of the exact layers (LGCN_AUX_STREAMS, 1..7): 3 (parts 0 and 1 and the
-    chain rows beside the caller's stream) with HIP's 4 hardware queues; 7 (a second lane of
-    half-layers: its main stream + its own 3, lgcn_sched_create) when GPU_MAX_HW_QUEUES >= 8
-    gives every stream a queue. At N > 1 RCCL's stream competes for them (dist asks for fewer)."""
+    """Auxiliary streams of the exact layers (LGCN_AUX_STREAMS, 1..7; default 7: parts 0 and 1
+    and the chain rows beside the caller's stream, plus a second lane of half-layers — its main
+    stream and its own 3, lgcn_sched_create). HIP keeps a pool of hardware queues per stream
+    priority (GPU_MAX_HW_QUEUES each, default 4): the caller's stream and aux 0..2 take the
+    normal-priority queues, the second lane's four high-priority streams their own — measured
+    at C3, the two lanes run as fast under HIP's default 4 queues as under 8 (17.08 vs 17.17 ms,
+    round 4), so the default needs no environment change and main.py gets the two lanes."""
     v = os.environ.get("LGCN_AUX_STREAMS", "")
-    n = int(v) if v else (7 if hw_queues() >= 8 else 3)
+    n = int(v) if v else 7
     return max(1, min(7, n))
 
 
@@ -1087,6 +1090,15 @@ side_trace = None   # a list: the sided entry points append {(k, side): [(phase,
 side_timing = None  # a list: ... append {(k, side): (start, end)} around each half-layer kernel
 
 
+last_schedule = None  # the schedule of the latest propagation call (diagnostics, tests)
+
+
+def _note_schedule(sc, sided):
+    global last_schedule
+    n = sc.n_aux if sc is not None else 0
+    last_schedule = {"sided": sided, "aux_streams": n, "lanes": 2 if sided and n >= 4 else 1}
+
+
 def use_sides(graph, layer_events=None, kernel_events=None):
     """The bipartite schedule runs when the graph is side-ordered (graph_from_coo with sides)
     and no per-layer events are asked for (a layer has no single boundary in it)."""
@@ -1137,6 +1149,7 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
             plans, _ = _side_plans(graph, d, hub_threshold, hub_mode, emu_min,
                                    _aligned16(segments))
             sc = sched_for(dev, _capture_aux(dev))
+            _note_schedule(sc, True)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
             try:
@@ -1231,6 +1244,7 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
                                    live=nz is not None)
             sc = sched_for(dev, _capture_aux(dev))
+            _note_schedule(sc, True)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             try:
                 _check(lib.lgcn_propagate_backward_sides(

@@ -157,3 +157,22 @@ def test_featsplit_shards_on_two_lanes(gpu_device, monkeypatch, brand_graph, P):
                       .cpu().numpy())
     assert np.array_equal(np.concatenate(cols, 1), want)
     assert np.array_equal(np.concatenate(cols_b, 1), want_g)
+
+
+def test_default_environment_runs_two_lanes(gpu_device, monkeypatch, brand_graph):
+    """What main.py gets (models/lightgcn.py forward under HIP's default hardware queues, no
+    LGCN_* stream knob): the drop-in forward runs the two-lane schedule with 7 aux streams (the
+    second lane's high-priority streams take their own queue pool), bitwise."""
+    import os
+    monkeypatch.delenv("LGCN_AUX_STREAMS", raising=False)
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    assert os.environ.get("GPU_MAX_HW_QUEUES") in (None, "", "4"), "not the default environment"
+    assert engine.n_aux_streams() == 7
+    r, c, v, n = brand_graph
+    adj = _adj(r, c, v, n, gpu_device)
+    e0 = _e0(np.random.default_rng(12), "xavier", n, 64)
+    w = _segs(e0, gpu_device)
+    out = engine.propagate_blocks(adj, w, 3, hub_threshold=128)
+    assert engine.last_schedule == {"sided": True, "aux_streams": 7, "lanes": 2}
+    got = torch.cat([o.detach() for o in out]).cpu().numpy()
+    assert np.array_equal(got, oracle.forward(r, c, v, e0, 3))

@@ -14,7 +14,6 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import bench  # noqa: E402
 from gcn_recommendation_amd import engine  # noqa: E402
 

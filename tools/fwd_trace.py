@@ -14,7 +14,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", os.environ.get("LGCN_HW_QUEUES", "") or "8")
+if os.environ.get("LGCN_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LGCN_HW_QUEUES"]
 import bench  # noqa: E402
 from gcn_recommendation_amd import engine  # noqa: E402
 

@@ -29,7 +29,10 @@ static void handler(int sig, siginfo_t* si, void* ctx) {
     raise(sig);
 }
 
-__attribute__((constructor)) static void install(void) {
+void segv_install(void);
+__attribute__((constructor)) static void install(void) { segv_install(); }
+
+void segv_install(void) {
     struct sigaction sa;
     memset(&sa, 0, sizeof sa);
     sa.sa_sigaction = handler;
