@@ -224,6 +224,99 @@ def val_split(u, i):
     return u[~val], i[~val], u[val], i[val]
 
 
+def bench_recall_trained_c3(dev, steps, k=20, batch=2048, n_val=2048):
+    """A Recall@20 at C3 (BASELINE configs[2] shape) that carries information: the Books-shape
+    power-law interactions with main.py's validation split held out (main.py:201-203), Â built
+    on the device from the train rows (main.py:282-336), the drop-in LightGCN trained for `steps`
+    BPR batches of main.py's loop (main.py:479-531: shuffled (user, pos) batches of 2048,
+    negatives rejected against the user's train items, bpr_loss_reg, Adam lr=1e-3) through the
+    engine. The trained weights are propagated by the engine (exact plan) and by the reference
+    CPU path (torch.sparse.mm COO, oracle/), and both tables are scored with main.py's evaluate
+    (oracle restatement) on n_val sampled validation users; the fused top-K kernel scores the
+    engine's table too."""
+    from gcn_recommendation_amd import evaluate as E
+    from gcn_recommendation_amd.loss import bpr_loss_reg
+    from models.lightgcn import LightGCN
+    from oracle import oracle
+    cfg = CONFIGS["c3"]
+    U, I, d, K = cfg["users"], cfg["items"], cfg["d"], cfg["K"]
+    t_all = time.time()
+    u, i = graph.powerlaw_interactions(U, I, cfg["interactions"], cfg["seed"])
+    tu, ti, vu, vi = val_split(u, i)
+    del u, i
+    adj = graph.build_norm_adj_device(tu, ti, U, I, 0, use_brand=False, device=dev)
+
+    class Cfg:
+        embedding_dim, n_layers, debug = d, K, False
+    import contextlib
+    import io
+    torch.manual_seed(42)
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = LightGCN(U, I, 0, Cfg()).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    train_keys = np.unique(tu * np.int64(I) + ti)
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(tu.size)
+    loss = None
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for st in range(steps):
+        b = perm[st * batch:(st + 1) * batch]
+        bu, bp = tu[b], ti[b]
+        bn = rng.integers(0, I, b.size)
+        while True:  # rejection against the user's train items (BPRDataset, main.py:357-363)
+            key = bu * np.int64(I) + bn
+            pos = np.minimum(np.searchsorted(train_keys, key), train_keys.size - 1)
+            hit = train_keys[pos] == key
+            if not hit.any():
+                break
+            bn[hit] = rng.integers(0, I, int(hit.sum()))
+        users, pi, ni = (torch.from_numpy(x).to(dev) for x in (bu, bp, bn))
+        opt.zero_grad()
+        fu, fi, _, u0, i0 = model(adj, use_brand=False)
+        loss = bpr_loss_reg(fu[users], fi[pi], fi[ni], u0[users], i0[pi], i0[ni], 1e-4)
+        loss.backward()
+        opt.step()
+    torch.cuda.synchronize()
+    train_s = time.time() - t0
+    del opt, train_keys
+    # validation users (sampled) and their train items (the -1e10 mask of main.py:422-424)
+    sel = np.sort(np.random.default_rng(1).choice(vu.size, min(n_val, vu.size), replace=False))
+    su, si = vu[sel], vi[sel]
+    m = np.isin(tu, su)
+    mu, mi = tu[m], ti[m]
+    with torch.no_grad():
+        fu, fi, _, _, _ = model(adj)
+        ego = torch.cat([model.user_embedding.weight, model.item_embedding.weight]).cpu()
+        gpu = torch.cat([fu, fi]).cpu()
+        mrow, mit = E.mask_csr(mu, mi, U)
+        _, top = E.topk_fused(fu, fi, su, mrow, mit, k)
+    del model
+    torch.cuda.empty_cache()
+    ref = oracle.reference_forward_torch(adj.cpu(), ego, K)
+    rec_cpu = oracle.evaluate(ref[:U], ref[U:], su, si, mu, mi, k, batch_size=128)
+    rec_gpu = oracle.evaluate(gpu[:U], gpu[U:], su, si, mu, mi, k, batch_size=128)
+    hit = top.cpu().numpy() == si[:, None]
+    found = hit.any(1)
+    ndcg = np.where(found, 1.0 / np.log2(hit.argmax(1) + 2), 0.0)
+    return {"config": "C3 power-law 10.3M x 4.4M x 29.5M, d=64, K=3; val = main.py:201-203's "
+                      "split (groupby-rank 1: each user's first row)",
+            "train_steps": steps, "batch": batch, "train_s": round(train_s, 1),
+            "loss_last": float(loss.item()) if loss is not None else None,
+            "val_users_scored": int(su.size), "val_users_total": int(vu.size),
+            "recall20_gpu": rec_gpu[0], "ndcg20_gpu": rec_gpu[1],
+            "recall20_cpu_ref": rec_cpu[0], "ndcg20_cpu_ref": rec_cpu[1],
+            "identical": rec_gpu == rec_cpu,
+            "embeddings_bitwise_equal": bool(torch.equal(gpu.view(torch.int32),
+                                                         ref.view(torch.int32))),
+            "fused_topk": {"recall20": float(found.mean()), "ndcg20": float(ndcg.mean())},
+            "wall_s": round(time.time() - t_all, 1),
+            "what": "weights trained on the GPU through the engine for `train_steps` BPR batches; "
+                    "the same weights propagated by the engine and by the reference CPU path, "
+                    "both scored by main.py's evaluate (oracle restatement) on sampled "
+                    "validation users; fused_topk = the engine's lgcn_score_topk"}
+
+
 def bench_recall_trained(dev, epochs, k=20, batch=2048):
     """Recall@20 / NDCG@20 that mean something (random-init embeddings give ~0 by construction):
     the C2 power-law graph (BASELINE configs[1] shape) with main.py's validation split held out
@@ -316,6 +409,8 @@ def main():
     ap.add_argument("--recall-users", type=int, default=2048)
     ap.add_argument("--recall-epochs", type=int, default=10,
                     help="epochs of C2 training for the trained Recall@20 parity (0: skip)")
+    ap.add_argument("--recall-steps-c3", type=int, default=300,
+                    help="BPR steps of training on the C3 graph for a Recall@20 at C3 (0: skip)")
     ap.add_argument("--train-steps", type=int, default=5,
                     help="also time main.py's training step (forward+BPR+backward+Adam)")
     ap.add_argument("--mode", default="featsplit", choices=["rowpart", "featsplit"],
@@ -754,6 +849,10 @@ def main():
                                       "Recall@20)"}
     if args.recall_epochs > 0 and args.config == "c3" and not args.no_cpu_baseline:
         result["recall20_trained"] = bench_recall_trained(dev, args.recall_epochs)
+    if args.recall_steps_c3 > 0 and args.config == "c3" and not args.no_cpu_baseline:
+        out = None
+        torch.cuda.empty_cache()
+        result["recall20_trained_c3"] = bench_recall_trained_c3(dev, args.recall_steps_c3)
     print(json.dumps(result), flush=True)
 
 

@@ -329,10 +329,12 @@ __device__ unsigned long long g_emu_stats[8];
 __device__ unsigned long long g_emu_row_stats[256][4];
 #endif
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
-// timing experiments only: 1 = failing blocks are not resolved (value kept), 2 = every block
-// translates
 __device__ int g_emu_mode;
-#define LGCN_EMU_FORCE(f) do { if (g_emu_mode == 2) (f) = true; } while (0)
+// timing experiments only: 1 = failing blocks are not resolved (value kept), 2 = every block
+// translates, 3 = every block is resolved, 4 = every block fails and is not resolved, 5 = as 4
+// with no slot fetched
+#define LGCN_EMU_FORCE(f) do { if (g_emu_mode == 2) (f) = true; \
+                               if (g_emu_mode >= 3) (f) = false; } while (0)
 #else
 #define LGCN_EMU_FORCE(f) ((void)0)
 #endif
@@ -398,6 +400,26 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                  "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+}
+
+// s_waitcnt vmcnt(m) for the largest m in {32, 16, 8, 4, 2, 1, 0} not above a wave-uniform n:
+// at most n younger operations may stay outstanding, a few of them may be waited for too — three
+// compares instead of wait_vm_upto's branch tree, on the walk's per-block path
+__device__ __forceinline__ void wait_vm_coarse(int n) {
+    if (n >= 63) return;
+    if (n >= 16) {
+        if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else if (n >= 4) {
+        if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (n >= 2) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else if (n == 1) {
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n (at most n of this wave's vector-memory operations
@@ -697,7 +719,11 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         const int lo = m.x >> wc, hi = -((-m.y) >> wc);
         const int alo = neg ? -hi : lo, ahi = neg ? -lo : hi;
         const int mg = ((hi - lo) >> 3) + 256;
-        const bool ok = ident || (inw && M + alo >= kLB + mg && M + ahi <= kHB - mg);
+        bool ok = ident || (inw && M + alo >= kLB + mg && M + ahi <= kHB - mg);
+        LGCN_EMU_FORCE(ok);
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+        if (g_emu_mode == 5) ok = true;  // nothing predicted (and nothing fetched: mode 5)
+#endif
         pred = __ballot(act && !ok);
 #ifdef LGCN_WALK_NO_REFILL  // build-time A/B: the first NS only, the rest fetched on demand
         {
@@ -776,22 +802,30 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
             PH_MARK(1);
             PH_COUNT(8, 1);
             PH_COUNT(9, __builtin_popcountll(pred_c));
+#ifdef LGCN_WALK_FINE_WAIT
             wait_vm_upto(nvm - stamp_c);  // chunk ch's first slots have landed
+#else
+            wait_vm_coarse(nvm - stamp_c);  // chunk ch's first slots have landed
+#endif
             PH_MARK(2);
             int from = 0;
+            bool direct = false;  // block `from` is re-run without a test (a predicted run)
             while (true) {
-                int incl, dm;
-                const unsigned long long bad = test(ab, from, nb, buf, mc, false, incl, dm);
-                const int f = bad ? (int)__builtin_ctzll(bad) : nb;
-                // blocks [from, f) translate: their mantissa changes add to the bits
-                const int tv = f < nb ? incl - dm : incl;
-                ab += (uint32_t)__builtin_amdgcn_readlane(tv, f < nb ? f : 63);
-                PH_MARK(3);
-                EMU_STAT(0, f - from);
+                int f = from;
+                if (!direct) {
+                    int incl, dm;
+                    const unsigned long long bad = test(ab, from, nb, buf, mc, false, incl, dm);
+                    f = bad ? (int)__builtin_ctzll(bad) : nb;
+                    // blocks [from, f) translate: their mantissa changes add to the bits
+                    const int tv = f < nb ? incl - dm : incl;
+                    ab += (uint32_t)__builtin_amdgcn_readlane(tv, f < nb ? f : 63);
+                    PH_MARK(3);
+                    EMU_STAT(0, f - from);
 #ifdef LGCN_EMU_STATS
-                n_fast += f - from;
+                    n_fast += f - from;
 #endif
-                if (f >= nb) break;
+                    if (f >= nb) break;
+                }
                 // refills: the predicted blocks before f are done, their slots take the next
                 // predicted ones (at most NS ahead of f, so f's own slot is kept)
                 const int done = __builtin_popcountll(pred_c & ((1ull << f) - 1ull));
@@ -813,13 +847,21 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                 if ((pred_c >> f) & 1ull) {
                     sl = buf * NS + done % NS;
                     if (done >= NS) {  // a refill: wait for its own fetch only
+#ifdef LGCN_WALK_FINE_WAIT
                         wait_vm_upto(nvm - __builtin_amdgcn_readlane(stamp, done));
+#else
+                        wait_vm_coarse(nvm - __builtin_amdgcn_readlane(stamp, done));
+#endif
                         PH_MARK(5);
                     }
                 } else {  // not predicted: fetched now into the spare slot
                     sl = spare;
                     EMU_STAT(3, 1);
                     PH_COUNT(11, 1);
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+                    if (g_emu_mode == 5) {
+                    } else
+#endif
                     if (staged) {
                         fetch(fb + kb, sl);
                         nvm += 2;
@@ -844,7 +886,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                     PH_MARK(5);
                 }
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
-                if (g_emu_mode != 1)
+                if (g_emu_mode != 1 && g_emu_mode < 4)
 #endif
                     ab = resolve_block(slot_v(sl), slot_x(sl), n, ab, max_it, iters);
                 PH_MARK(4);
@@ -855,6 +897,14 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
 #endif
                 from = f + 1;
                 if (from >= nb) break;
+                // the next block predicted to fail too (runs of them: the chain value wanders
+                // near zero or along a binade boundary): re-run it without a test — a re-run
+                // is the reference's chain, exact whether or not the block would translate, and
+                // it costs about what the test does (~0.6 us either way)
+                direct = (pred_c >> from) & 1ull;
+#if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
+                if (g_emu_mode == 2) direct = false;
+#endif
             }
             // rotate: chunk ch + 2's table into chunk ch's buffer, chunk ch + 3's loads
             if (ch + 2 < nch) {

@@ -147,16 +147,21 @@ def walk_timing(g, segs, d, thr, emu_min):
     has_stats = has_modes and hasattr(lib, "lgcn_emu_stats")
     if has_modes:
         lib.lgcn_emu_set_mode.argtypes = [ctypes.c_int]
-    for mode in ([0, 1, 2] if has_modes else [0]):
+    for mode in ([0, 1, 2, 3, 4, 5] if has_modes else [0]):
         if has_modes:
             lib.lgcn_emu_set_mode(mode)
             torch.cuda.synchronize()
         if has_stats:
             stats(lib)
             row_stats(lib, hp, d, quiet=True)
+            if hasattr(lib, "lgcn_emu_phase"):
+                buf = (ctypes.c_ulonglong * 16)()
+                lib.lgcn_emu_phase(buf)  # reset
         if has_modes:
-            print(f" walker mode {mode} (0 normal, 1 re-run blocks skip the chain, 2 all translate)")
-        for lo, hi in ((0, 1), (1, 2), (0, 8), (8, hp.n_emu_rows), (0, hp.n_emu_rows)):
+            print(f" walker mode {mode} (0 normal, 1 re-run blocks skip the chain, 2 all translate, "
+                  f"3 all resolved, 4 all fail, none resolved)")
+        for lo, hi in ((0, 1), (1, 2), (0, 8)) + (((8, hp.n_emu_rows), (0, hp.n_emu_rows))
+                                                if mode == 0 else ()):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             assert lib.lgcn_emu_walk(engine._ptr(g.edges), plan.emu_blocks,
@@ -169,6 +174,7 @@ def walk_timing(g, segs, d, thr, emu_min):
             if has_stats and (lo, hi) == (0, 1):
                 print("   row 0 decisions:", stats(lib), flush=True)
                 row_stats(lib, hp, d, quiet=True)
+                phase_stats(lib)
     if has_modes:
         lib.lgcn_emu_set_mode(0)
 
