@@ -460,7 +460,7 @@ int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int
     const int64_t b1 = (chain_max + B - 1) / B;                  // chain rows: <= b1 blocks
     const int64_t b0 = std::max<int64_t>(part0_blocks, b1);      // part 0: > b0 blocks
     int64_t nb_total = 0;
-    int32_t pr[2] = {0, 0}, pb[2] = {0, 0};
+    int32_t pr[2] = {0, 0}, pb[2] = {0, 0}, pm[2] = {0, 0};
     for (size_t i = 0; i < em.size(); ++i) {
         const int32_t s = em[i];
         const int64_t beg = rowptr_host[s], deg = (int64_t)rowptr_host[s + 1] - beg;
@@ -468,6 +468,9 @@ int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int
         if (nb_total + nb > INT32_MAX) return LGCN_EINVAL;
         if (nb > b0) pr[0] = (int32_t)(i + 1), pb[0] = (int32_t)(nb_total + nb);
         if (nb > b1) pr[1] = (int32_t)(i + 1), pb[1] = (int32_t)(nb_total + nb);
+        // the first (longest) row of each part
+        if (nb > b0 && !pm[0]) pm[0] = (int32_t)nb;
+        if (nb <= b0 && nb > b1 && !pm[1]) pm[1] = (int32_t)nb;
         if (rows_host) {
             rows_host[i].row = row_ids_host ? row_ids_host[s] : s;
             rows_host[i].first_block = (int32_t)nb_total;
@@ -490,6 +493,8 @@ int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int
     plan->emu_part_blocks[0] = pb[0];
     plan->emu_part_blocks[1] = pb[1];
     plan->emu_scratch_blocks = pb[1];
+    plan->emu_part_max_blocks[0] = pm[0];
+    plan->emu_part_max_blocks[1] = pm[1];
     return 0;
 }
 
@@ -782,6 +787,7 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
 // The concurrent schedule of an exact layer (lgcn_sched_create): auxiliary streams the emulated
 // and chain rows run on beside the layer kernel, and the events that fork them from the caller's
 // stream and join them back (graph-capture safe: a captured fork/join is a graph dependency).
+#define LGCN_SCHED_MAX_PIECES 4
 struct lgcn_sched {
     hipStream_t aux[3];
     int n_aux;
@@ -804,6 +810,16 @@ struct lgcn_sched {
     // the longest rows' walk starts before the layer kernel floods the chip
     int blocks_first;
     hipEvent_t blocks_done;
+    // LGCN_SCHED_MEAN_EARLY: a final (mean) half-layer forks its block passes before it waits for
+    // the other lane's layer K-1; only the kernels that write Y wait (`late`, set per half-layer)
+    int mean_early;
+    hipEvent_t late;
+    // LGCN_SCHED_PIECES: parts 0 and 1 run their block pass and walk in `pieces` chunk windows
+    // (block pass windows on the caller's stream, piece_ev[part][j] after window j; the walk of
+    // window j waits for it), so a walk starts after the block pass of its first chunks
+    int pieces;
+    hipEvent_t piece_ev[2][LGCN_SCHED_MAX_PIECES];
+    int chains_first;  // LGCN_SCHED_CHAINS_FIRST
 };
 
 namespace {
@@ -862,6 +878,10 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     // walked rows read the block-pass scratch, which must cover their blocks
     if ((chains || live ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
         return LGCN_EINVAL;
+    // the operands of the epilogue are ready once `late` fires: without the concurrent block
+    // passes below, everything waits for it
+    if (sc && sc->late && (live || ne == 0))
+        if (int e = herr(hipStreamWaitEvent(s, sc->late, 0))) return e;
     hipEvent_t* tr = sc ? sc->trace : nullptr;
     auto mark = [&](int k, hipStream_t st) -> int {
         return tr && tr[k] ? herr(hipEventRecord(tr[k], st)) : 0;
@@ -953,30 +973,83 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     if (int e = herr(hipEventRecord(sc->fork, s))) return e;
     for (int i = 0; i < na; ++i)
         if (int e = herr(hipStreamWaitEvent(sc->aux[i], sc->fork, 0))) return e;
+    // pieced parts (sc->pieces > 1): chunk windows [wc[j], wc[j + 1]) — 0, 4, 16, 64, ...
+    // chunks, the last window open — block-passed on `s` window by window, both parts
+    // interleaved, each window's walk on the part's stream after its window's event
+    const int np = std::min(sc->pieces, LGCN_SCHED_MAX_PIECES);
+    auto pieced = [&](int i) {
+        return np > 1 && i < 2 && parts[i].r1 > parts[i].r0 && p.emu_part_max_blocks[i] > 0 &&
+               parts[i].r1 - parts[i].r0 <= 65535;
+    };
+    auto wchunk = [&](int j) { return j <= 0 ? 0 : j >= np ? INT32_MAX : 1 << (2 * j); };
+    auto wblock = [&](int i, int j) {  // first block of window j's chunks (block 0 in window 0)
+        const int64_t c = wchunk(j);
+        return (int32_t)std::min<int64_t>(c == 0 ? 0 : 1 + 64 * c, p.emu_part_max_blocks[i]);
+    };
     // block passes first (the walk of part 0 starts as soon as its own is done), then the layer
     // kernel, then the walks and the chains
     for (int i = 0; i < 3; ++i)
-        if (i < 2 || !chains) {
+        if ((i < 2 || !chains) && !pieced(i)) {
             if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, nullptr, aux_of(i)))
                 return e;
             if (i < 2)
                 if (int e = mark(1 + i, aux_of(i))) return e;
         }
-    if (sc->blocks_first && sc->blocks_done && parts[0].b1 > parts[0].b0) {
+    for (int j = 0; j < np; ++j)
+        for (int i = 0; i < 2; ++i) {
+            if (!pieced(i) || wblock(i, j) >= wblock(i, j + 1)) continue;
+            if (int e = lgcn_emu_blocks_rows(edges, p.emu_blocks, p.emu_rows + parts[i].r0,
+                                             parts[i].r1 - parts[i].r0, wblock(i, j),
+                                             wblock(i, j + 1), x, xdiv, x_nz, d, p.emu_rel,
+                                             p.emu_meta, p.emu_stage, nullptr, s))
+                return e;
+            if (int e = herr(hipEventRecord(sc->piece_ev[i][j], s))) return e;
+            if (wblock(i, j + 1) >= p.emu_part_max_blocks[i])
+                if (int e = mark(1 + i, s)) return e;
+        }
+    // the block passes read X only; every kernel after them writes Y, whose epilogue operands are
+    // ready once `late` fires
+    if (sc->late) {
+        if (int e = herr(hipStreamWaitEvent(s, sc->late, 0))) return e;
+        for (int i = 0; i < na; ++i)
+            if (int e = herr(hipStreamWaitEvent(sc->aux[i], sc->late, 0))) return e;
+    }
+    if (sc->blocks_first && sc->blocks_done && parts[0].b1 > parts[0].b0 && !pieced(0)) {
         if (int e = herr(hipEventRecord(sc->blocks_done, aux_of(0)))) return e;
         if (int e = herr(hipStreamWaitEvent(s, sc->blocks_done, 0))) return e;
     }
+    // a layer that walks nothing (C3's user half-layers: a few short chain rows) runs its chains
+    // on `s` before the layer kernel (LGCN_SCHED_CHAINS_FIRST): launched on an aux stream they
+    // were dispatched only once the layer kernel's grid was (~3.5 ms at C3)
+    const bool chains_first = chains && sc->chains_first && parts[0].r1 == parts[0].r0 &&
+                              parts[1].r1 == parts[1].r0;
+    if (chains_first) {
+        if (int e = chain_rows(s)) return e;
+        if (int e = mark(4, s)) return e;
+    }
     if (int e = layer_kernel(s)) return e;
     if (int e = mark(3, s)) return e;
-    if (chains) {
+    if (chains && !chains_first) {
         if (int e = chain_rows(aux_of(2))) return e;
         if (int e = mark(4, aux_of(2))) return e;
     }
     for (int i = 0; i < 3; ++i)
         if (i < 2 || !chains) {
-            if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
-                                  nullptr, aux_of(i)))
+            if (pieced(i)) {
+                for (int j = 0; j < np && wblock(i, j) < wblock(i, j + 1); ++j) {
+                    if (int e = herr(hipStreamWaitEvent(aux_of(i), sc->piece_ev[i][j], 0)))
+                        return e;
+                    if (int e = lgcn_emu_walk_chunks(
+                            edges, p.emu_blocks, p.emu_rows + parts[i].r0,
+                            parts[i].r1 - parts[i].r0, p.emu_rel, p.emu_meta, p.emu_stage, x,
+                            xdiv, x_nz, y, ldy, d, &ep, slots[i], nullptr, wchunk(j),
+                            wchunk(j + 1), aux_of(i)))
+                        return e;
+                }
+            } else if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep,
+                                         slots[i], nullptr, aux_of(i))) {
                 return e;
+            }
             if (i < 2)
                 if (int e = mark(5 + i, aux_of(i))) return e;
         }
@@ -987,6 +1060,18 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     }
     return mark(7, s);
 }
+
+#ifdef LGCN_CAPTURE_DEBUG
+// capture-crash bisection (variant build): LGCN_CAPTURE_EXP bits — 1: lane 1's aux streams are
+// not forked from the caller's stream, 2: nor joined into it, 4: lane 0 keeps one aux stream,
+// 8: lane 1 keeps its aux streams under a capture
+int cap_exp() {
+    static const int v = getenv("LGCN_CAPTURE_EXP") ? atoi(getenv("LGCN_CAPTURE_EXP")) : 0;
+    return v;
+}
+#else
+constexpr int cap_exp() { return 0; }
+#endif
 
 // The bipartite schedule (lgcn_propagate_*_sides): a lane = the stream its half-layers' layer
 // kernels run on + the schedule view whose aux streams take their emulated / chain rows.
@@ -1000,7 +1085,8 @@ struct Lane {
 int half_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
                int32_t n, int32_t split, const lgcn_hub_plan_t* plans, int k, int side,
                const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y, int32_t d,
-               const lgcn_epilogue_t& ep, const lgcn_sched* sc, const Lane& L) {
+               const lgcn_epilogue_t& ep, const lgcn_sched* sc, const Lane& L,
+               hipEvent_t late = nullptr) {
     const int32_t s0 = side ? split : 0, s1 = side ? n : split;
     if (s1 <= s0) return 0;
     const int h = (k - 1) * 2 + side;
@@ -1012,30 +1098,44 @@ int half_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
         v.t0 = tm ? tm[2 * h] : nullptr;
         v.t1 = tm ? tm[2 * h + 1] : nullptr;
         v.trace = sc && sc->trace_sides ? sc->trace_sides + h * 8 : nullptr;
+        v.late = late;
+        if ((cap_exp() & 4) && L.view == sc && v.n_aux > 1) v.n_aux = 1;
         vp = &v;
+    } else if (late) {
+        if (int e = herr(hipStreamWaitEvent(L.main, late, 0))) return e;
     }
     return plan_layer(rowptr + s0, edges, row_ids + s0, s1 - s0, plans[2 * side + (k & 1)], x,
                       xdiv, x_nz, y, d, d, ep, vp, L.main);
 }
 
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
 // The two lanes: lane 1 on its own streams when the schedule has them, else both lanes share
 // the caller's stream (half-layers then run in layer order, each still overlapped inside).
-bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2]) {
+// While `s` is being captured into a HIP graph, lane 1 runs its half-layers on its main stream
+// alone (parts in order): a capture that forks lane 1's own aux streams as well crashes
+// hipStreamEndCapture on this ROCm (segfault; the same lanes without them capture and replay
+// bitwise, tests/test_gpu_sides.py).
+bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2], bool& l1_aux) {
     lanes[0] = Lane{s, sc};
     const bool two = sc && sc->lane1;
-    lanes[1] = two ? Lane{sc->lane1_main, sc->lane1->n_aux ? sc->lane1 : nullptr} : lanes[0];
+    l1_aux = two && sc->lane1->n_aux > 0 && (!capturing(s) || (cap_exp() & 8));
+    lanes[1] = two ? Lane{sc->lane1_main, l1_aux ? sc->lane1 : nullptr} : lanes[0];
     return two;
 }
 
 // Lane 1 forked from the caller's stream: its main stream AND its aux streams wait on `s` first
 // (a stream captured by way of another forked stream — origin -> A -> B — crashes HIP's
 // hipStreamEndCapture on this ROCm; every stream entering the capture from the origin is fine).
-int fork_lanes(const lgcn_sched* sc, bool two, hipStream_t s) {
+int fork_lanes(const lgcn_sched* sc, bool two, bool l1_aux, hipStream_t s) {
     if (!two) return 0;
     if (int e = herr(hipEventRecord(sc->lane_fork, s))) return e;
     if (int e = herr(hipStreamWaitEvent(sc->lane1_main, sc->lane_fork, 0))) return e;
     const lgcn_sched* l1 = sc->lane1;
-    for (int i = 0; i < l1->n_aux; ++i)
+    for (int i = 0; i < (l1_aux && !(cap_exp() & 1) ? l1->n_aux : 0); ++i)
         if (int e = herr(hipStreamWaitEvent(l1->aux[i], sc->lane_fork, 0))) return e;
     return 0;
 }
@@ -1043,12 +1143,12 @@ int fork_lanes(const lgcn_sched* sc, bool two, hipStream_t s) {
 // Lane 1 back into the caller's stream: its main stream and (already joined into that) its aux
 // streams, each also joined into `s` directly — a captured stream forked from another forked
 // stream must still end joined into the capture's origin for hipStreamEndCapture.
-int join_lanes(const lgcn_sched* sc, bool two, hipStream_t s) {
+int join_lanes(const lgcn_sched* sc, bool two, bool l1_aux, hipStream_t s) {
     if (!two) return 0;
     if (int e = herr(hipEventRecord(sc->lane_join, sc->lane1_main))) return e;
     if (int e = herr(hipStreamWaitEvent(s, sc->lane_join, 0))) return e;
     const lgcn_sched* l1 = sc->lane1;
-    for (int i = 0; i < l1->n_aux; ++i) {
+    for (int i = 0; i < (l1_aux && !(cap_exp() & 2) ? l1->n_aux : 0); ++i) {
         if (int e = herr(hipEventRecord(l1->join[i], l1->aux[i]))) return e;
         if (int e = herr(hipStreamWaitEvent(s, l1->join[i], 0))) return e;
     }
@@ -1101,6 +1201,8 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
     int e = mk(&sc->fork);
     for (int i = 0; i < n0 && !e; ++i) e = mk(&sc->join[i]);
     if (!e) e = mk(&sc->blocks_done);
+    for (int i = 0; i < 2 && !e; ++i)
+        for (int j = 0; j < LGCN_SCHED_MAX_PIECES && !e; ++j) e = mk(&sc->piece_ev[i][j]);
     if (!e && n_aux >= 4) {
         sc->lane1_main = reinterpret_cast<hipStream_t>(aux_streams[3]);
         sc->lane1 = new (std::nothrow) lgcn_sched();
@@ -1115,6 +1217,8 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
             e = mk(&l1->fork);
             for (int i = 0; i < l1->n_aux && !e; ++i) e = mk(&l1->join[i]);
             if (!e) e = mk(&l1->blocks_done);
+            for (int i = 0; i < 2 && !e; ++i)
+                for (int j = 0; j < LGCN_SCHED_MAX_PIECES && !e; ++j) e = mk(&l1->piece_ev[i][j]);
             if (!e) e = mk(&sc->lane_fork);
             if (!e) e = mk(&sc->lane_join);
             for (int i = 0; i < 2 && !e; ++i) e = mk(&sc->cross[i]);
@@ -1132,6 +1236,9 @@ int lgcn_sched_destroy(lgcn_sched_t* sc) {
     if (!sc) return 0;
     if (sc->fork) (void)hipEventDestroy(sc->fork);
     if (sc->blocks_done) (void)hipEventDestroy(sc->blocks_done);
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < LGCN_SCHED_MAX_PIECES; ++j)
+            if (sc->piece_ev[i][j]) (void)hipEventDestroy(sc->piece_ev[i][j]);
     for (int i = 0; i < 3; ++i)
         if (sc->join[i]) (void)hipEventDestroy(sc->join[i]);
     hipEvent_t* own[] = {&sc->lane_fork, &sc->lane_join, &sc->cross[0], &sc->cross[1]};
@@ -1170,6 +1277,18 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
         case LGCN_SCHED_BLOCKS_FIRST:
             sc->blocks_first = value != 0;
             if (sc->lane1) sc->lane1->blocks_first = value != 0;
+            return 0;
+        case LGCN_SCHED_MEAN_EARLY:
+            sc->mean_early = value != 0;
+            return 0;
+        case LGCN_SCHED_CHAINS_FIRST:
+            sc->chains_first = value != 0;
+            if (sc->lane1) sc->lane1->chains_first = value != 0;
+            return 0;
+        case LGCN_SCHED_PIECES:
+            if (value < 0 || value > LGCN_SCHED_MAX_PIECES) return LGCN_EINVAL;
+            sc->pieces = (int)value;
+            if (sc->lane1) sc->lane1->pieces = (int)value;
             return 0;
         case LGCN_SCHED_TIMING_SIDES:
             sc->timing_sides = reinterpret_cast<hipEvent_t*>(value);
@@ -1246,8 +1365,9 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
     if (K == 0) return scale_rows(emb, n, d, 1.0f, out, d, s);
     if (int e = check_sides(rowptr, row_ids, n, split, plans)) return e;
     Lane lanes[2];
-    const bool two = make_lanes(sched, s, lanes);
-    if (int e = fork_lanes(sched, two, s)) return e;  // lane 1 starts where `s` is (E0 ready)
+    bool l1_aux = false;
+    const bool two = make_lanes(sched, s, lanes, l1_aux);
+    if (int e = fork_lanes(sched, two, l1_aux, s)) return e;  // lane 1 starts where `s` is (E0 ready)
     for (int k = 1; k <= K; ++k) {
         const lgcn_rows_t x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
         lgcn_epilogue_t ep;
@@ -1269,17 +1389,23 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
         // only; the two sides of one layer are independent)
         for (int side = 1; side >= 0; --side) {
             const Lane& L = lanes[(k + side + K) & 1];
-            // the mean of a side reads its layer K-1, computed on the other lane
-            if (two && k == K && K >= 2)
-                if (int e = herr(hipStreamWaitEvent(L.main, sched->cross[side], 0))) return e;
+            // the mean of a side reads its layer K-1, computed on the other lane: the half-layer
+            // waits for it — or, with MEAN_EARLY, only its kernels that write Y do
+            hipEvent_t late = nullptr;
+            if (two && k == K && K >= 2) {
+                if (sched->mean_early)
+                    late = sched->cross[side];
+                else if (int e = herr(hipStreamWaitEvent(L.main, sched->cross[side], 0)))
+                    return e;
+            }
             if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, x, 1.f,
-                                   nullptr, y, d, ep, sched, L))
+                                   nullptr, y, d, ep, sched, L, late))
                 return e;
             if (two && k == K - 1)
                 if (int e = herr(hipEventRecord(sched->cross[side], L.main))) return e;
         }
     }
-    return join_lanes(sched, two, s);
+    return join_lanes(sched, two, l1_aux, s);
 }
 
 int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
@@ -1294,8 +1420,9 @@ int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edge
     if (K > 1 && !work_h) return LGCN_EINVAL;
     if (int e = check_sides(rowptr, row_ids, n, split, plans)) return e;
     Lane lanes[2];
-    const bool two = make_lanes(sched, s, lanes);
-    if (int e = fork_lanes(sched, two, s)) return e;
+    bool l1_aux = false;
+    const bool two = make_lanes(sched, s, lanes, l1_aux);
+    if (int e = fork_lanes(sched, two, l1_aux, s)) return e;
     // as lgcn_propagate_backward; half-layer (k, side) reads layer k-1's other side, written on
     // the same lane, and overwrites (alternate buffers) layer k-2's same side, which only the
     // same lane's half-layer (k-1, other side) read
@@ -1319,7 +1446,7 @@ int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edge
         xdiv = 1.f;
         x_nz = nullptr;
     }
-    return join_lanes(sched, two, s);
+    return join_lanes(sched, two, l1_aux, s);
 }
 
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,

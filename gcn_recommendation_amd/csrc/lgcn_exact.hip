@@ -145,7 +145,9 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                                                    int4* __restrict__ ktab,
                                                    int4* __restrict__ meta,
                                                    float* __restrict__ stage,
-                                                   const lgcn_emu_row_t* __restrict__ live) {
+                                                   const lgcn_emu_row_t* __restrict__ live,
+                                                   const lgcn_emu_row_t* __restrict__ prows,
+                                                   int32_t k_lo, int32_t k_hi) {
     // steps gathered per sub-window (all in flight at once), two sub-windows in flight
 #ifndef LGCN_BLK_SW
 #define LGCN_BLK_SW 16
@@ -155,7 +157,16 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     const int lane = threadIdx.x;
     const int c = blockIdx.y * 64 + lane;
     const bool act = c < d;
-    const lgcn_emu_block_t blk = blocks[blockIdx.x];
+    // the block: blockIdx.x, or (row window, lgcn_emu_blocks_rows) block k_lo + blockIdx.x of
+    // row prows[blockIdx.z] when the row has it
+    int64_t bi = blockIdx.x;
+    if (prows) {
+        const lgcn_emu_row_t pr = prows[blockIdx.z];
+        const int32_t k = k_lo + (int32_t)blockIdx.x;
+        if (k >= min(k_hi, pr.n_blocks)) return;
+        bi = pr.first_block + k;
+    }
+    const lgcn_emu_block_t blk = blocks[bi];
     // a row the live-edge chains run (lgcn_live_rows flags it) needs no block pass
     if (live && live[blk.row].n_blocks) return;
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
@@ -191,9 +202,8 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     // stride scattered 64 half-written lines over L2 per instruction: ~60% of the pass's time.)
     constexpr int TP = 36;  // tile pitch in floats: 32 steps + 4 (ds_write_b128 conflict-free)
     __shared__ __attribute__((aligned(16))) float s_tile[64 * TP];
-    float* const st0 = stage ? stage + (int64_t)blockIdx.x * (d + 1) * LGCN_EMU_BLOCK : nullptr;
-    float* sv = stage && blockIdx.y == 0
-                    ? stage + ((int64_t)blockIdx.x * (d + 1) + d) * LGCN_EMU_BLOCK : nullptr;
+    float* const st0 = stage ? stage + bi * (d + 1) * LGCN_EMU_BLOCK : nullptr;
+    float* sv = stage && blockIdx.y == 0 ? stage + (bi * (d + 1) + d) * LGCN_EMU_BLOCK : nullptr;
     const bool staging = st0 && !LGCN_BLK_OFF(1);
     auto stage_sub = [&](const float (&xv)[SW], int part) {  // SW steps into the tile
         if (!staging) return;
@@ -278,7 +288,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
         rec = nrec;
     }
     if (!act) return;
-    const int64_t rc = (int64_t)blockIdx.x * d + c;
+    const int64_t rc = bi * d + c;
     // |T_j - S_j| <= j * ulp(max|T|) / 2 <= 128 * ulp(max|T|) for a block of <= 256 steps
     const float M = fmaxf(-tlo, thi);
     double err = 0.0;
@@ -359,7 +369,7 @@ __device__ unsigned long long g_emu_phase[16];
 #define LGCN_EMU_SLOTS 12   // default LDS slots per chunk for predicted resolve blocks
 // static LDS of k_emu_walk (two 16 x 64 translation tables, 8 KB) + (2 * slots + 1) 2-KB slots
 // within a CU's 160 KB; and a chunk's slot fetches (2 per slot) + the 5 table loads after them
-// within the 62 outstanding loads wait_vm_upto waits for
+// within the 63 outstanding loads a vmcnt wait can count
 #define LGCN_EMU_MAX_SLOTS 28
 
 // Inclusive prefix sum over the 64 lanes of a wave by DPP row shifts and row broadcasts (no LDS
@@ -402,42 +412,36 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
                  : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
 }
 
+// Two 1-KB LDS-DMAs to consecutive KB of LDS (dst, dst + 1024): one m0 save/restore.
+__device__ __forceinline__ void dma16x2(const void* g0, const void* g1, uint32_t dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g0), "v"(g1),
+                   "s"(__builtin_amdgcn_readfirstlane((int)dst)) : "memory", "scc");
+}
+
 // s_waitcnt vmcnt(m) for the largest m in {32, 16, 8, 4, 2, 1, 0} not above a wave-uniform n:
-// at most n younger operations may stay outstanding, a few of them may be waited for too — three
-// compares instead of wait_vm_upto's branch tree, on the walk's per-block path
+// at most n younger operations may stay outstanding, a few of them may be waited for too. The
+// walk's common cases (a refill NS blocks old, n ~ 2 NS) take one or two compares instead of a
+// branch tree over every count.
 __device__ __forceinline__ void wait_vm_coarse(int n) {
     if (n >= 63) return;
-    if (n >= 16) {
-        if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if (n >= 32) {
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    } else if (n >= 16) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else if (n >= 8) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else if (n >= 4) {
-        if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else if (n >= 2) {
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     } else if (n == 1) {
         asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform n (at most n of this wave's vector-memory operations
-// outstanding; they complete in issue order)
-__device__ __forceinline__ void wait_vm_upto(int n) {
-    switch (n) {
-#define LGCN_WV(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-        LGCN_WV(0) LGCN_WV(1) LGCN_WV(2) LGCN_WV(3) LGCN_WV(4) LGCN_WV(5) LGCN_WV(6) LGCN_WV(7)
-        LGCN_WV(8) LGCN_WV(9) LGCN_WV(10) LGCN_WV(11) LGCN_WV(12) LGCN_WV(13) LGCN_WV(14)
-        LGCN_WV(15) LGCN_WV(16) LGCN_WV(17) LGCN_WV(18) LGCN_WV(19) LGCN_WV(20) LGCN_WV(21)
-        LGCN_WV(22) LGCN_WV(23) LGCN_WV(24) LGCN_WV(25) LGCN_WV(26) LGCN_WV(27) LGCN_WV(28)
-        LGCN_WV(29) LGCN_WV(30) LGCN_WV(31) LGCN_WV(32) LGCN_WV(33) LGCN_WV(34) LGCN_WV(35)
-        LGCN_WV(36) LGCN_WV(37) LGCN_WV(38) LGCN_WV(39) LGCN_WV(40) LGCN_WV(41) LGCN_WV(42)
-        LGCN_WV(43) LGCN_WV(44) LGCN_WV(45) LGCN_WV(46) LGCN_WV(47) LGCN_WV(48) LGCN_WV(49)
-        LGCN_WV(50) LGCN_WV(51) LGCN_WV(52) LGCN_WV(53) LGCN_WV(54) LGCN_WV(55) LGCN_WV(56)
-        LGCN_WV(57) LGCN_WV(58) LGCN_WV(59) LGCN_WV(60) LGCN_WV(61) LGCN_WV(62)
-#undef LGCN_WV
-        default: break;  // >= 63: nothing to wait for
     }
 }
 
@@ -592,17 +596,18 @@ __device__ __forceinline__ uint32_t resolve_block(const float* __restrict__ sv,
     return a;
 }
 
-template <int MODE, int XD>
+template <int MODE, int XD, bool ISO>
 __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__ edges,
                                                  const lgcn_emu_block_t* __restrict__ blocks,
                                                  const lgcn_emu_row_t* __restrict__ rows,
                                                  const int4* __restrict__ ktab,
-                                                 const int4* __restrict__ meta,
+                                                 int4* __restrict__ meta,
                                                  const float* __restrict__ stage, lgcn_rows_t x,
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
                                                  lgcn_epilogue_t ep, int NS, int max_it,
-                                                 const lgcn_emu_row_t* __restrict__ live) {
+                                                 const lgcn_emu_row_t* __restrict__ live,
+                                                 int32_t ch_lo, int32_t ch_hi) {
     constexpr int CH = LGCN_EMU_CH;
     constexpr int B = LGCN_EMU_BLOCK;
     static_assert(CH == 64, "one lane per block of a chunk");
@@ -611,14 +616,15 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // 2 sets x NS slots (chunk c uses set c & 1) + one spare: a block's edge values, then its
     // X elements (dynamic LDS, sized at launch)
     extern __shared__ __attribute__((aligned(16))) float s_dyn[];
-    auto slot_v = [&](int i) { return s_dyn + i * 2 * B; };
-    auto slot_x = [&](int i) { return s_dyn + i * 2 * B + B; };
     const int lane = threadIdx.x;
     const int c = blockIdx.y;
 #ifdef LGCN_WALK_PRIO
     // issue priority over the co-resident waves of other kernels on this SIMD (build flag A/B)
     __builtin_amdgcn_s_setprio(LGCN_WALK_PRIO);
 #endif
+    // ISO: the wave holds the SIMD's whole register file (v255 and a255 claimed), so no other
+    // wave shares its issue slots — the walk is issue-bound on one wave
+    if constexpr (ISO) asm volatile("" ::: "v255", "a255");
     // a row the live-edge chains run (lgcn_live_rows flags it, aligned with `rows`) is theirs
     if (live && live[blockIdx.x].n_blocks) return;
     const lgcn_emu_row_t er = rows[blockIdx.x];
@@ -627,9 +633,16 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // block k of the row holds edges [row_beg + k * B, min(.. + B, row_end)) (plan_emulation)
     const int32_t row_beg = blocks[fb].beg;
     const int32_t row_end = blocks[fb + nb_all - 1].end;
-    // the chain value as its bits (wave-uniform); block 0's chain from +0 is the true chain
-    uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(meta[fb * d + c].w);
-    const int nch = (nb_all - 1 + CH - 1) / CH;  // chunks of blocks 1, 2, ...
+    // chunks of blocks 1, 2, ...; this launch walks chunks [ch_lo, ch_end) (a chunk window:
+    // lgcn_emu_walk_chunks), a row with none of them left has been written
+    const int nch_all = (nb_all - 1 + CH - 1) / CH;
+    if (ch_lo > 0 && nch_all <= ch_lo) return;
+    const int nch = min(nch_all, ch_hi);
+    // the chain value as its bits (wave-uniform): block 0's chain from +0 is the true chain; its
+    // meta word w also carries the value from one chunk window to the next (written below, read
+    // here: block 0's record is read by nothing else)
+    int* const carry = reinterpret_cast<int*>(meta + fb * d + c) + 3;
+    uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(*carry);
     const bool staged = stage != nullptr;
     const int spare = 2 * NS;
 #ifdef LGCN_EMU_STATS
@@ -736,9 +749,19 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         return (uint32_t)__builtin_amdgcn_readfirstlane(
             (int)__float_as_uint(__uint_as_float(pa) + tot));
     };
-    auto fetch = [&](int64_t bi, int slot) {  // block bi's staged values -> LDS slot (2 DMAs)
-        dma16(stage + (bi * (d + 1) + d) * B + 4 * lane, lds_byte(slot_v(slot)));
-        dma16(stage + (bi * (d + 1) + c) * B + 4 * lane, lds_byte(slot_x(slot)));
+    // Slots by LDS float offset from s_dyn: slot i at 2 B i (values, then X). The ring: lane k
+    // holds the offset of slot k % NS of set 0 — predicted block #k of a chunk lives there —
+    // read back by readlane, no division on the walk's per-block path.
+    const uint32_t lds0 = lds_byte(s_dyn);
+    const int ring = (lane % NS) * 2 * B;
+    const int set_off = NS * 2 * B;
+    // block kb of the row: its staged values at st_v + kb * (d + 1) B, column c at st_x + ...
+    const float* st_v = stage + ((fb * (d + 1)) + d) * B + 4 * lane;
+    const float* st_x = stage + ((fb * (d + 1)) + c) * B + 4 * lane;
+    const int64_t blk_stride = (int64_t)(d + 1) * B;
+    auto fetch = [&](int kb, int off) {  // block kb's staged values -> LDS at float offset off
+        const int64_t o = (int64_t)kb * blk_stride;
+        dma16x2(st_v + o, st_x + o, lds0 + 4u * (uint32_t)off);
     };
     // the first NS predicted blocks of chunk ch into slot set `set`; returns the predicted
     // blocks left for refills (nvm: this wave's vector-memory operations issued so far)
@@ -746,46 +769,47 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                            int& nvm) -> unsigned long long {
         unsigned long long m = pred;
         for (int s = 0; s < NS && m; ++s, m &= m - 1) {
-            fetch(fb + 1 + (int64_t)ch * CH + __builtin_ctzll(m), set * NS + s);
+            fetch(1 + ch * CH + __builtin_ctzll(m), (set * NS + s) * 2 * B);
             nvm += 2;
         }
         return m;
     };
-    if (nch > 0) {
+    if (nch > ch_lo) {
         Tab tn;
         int4 mc, mn = make_int4(0, 0, 0, 0);
         // vmcnt bookkeeping: nvm counts this wave's vector-memory operations (5 per table load,
         // 2 per block fetch); an operation stamped s has landed once at most nvm - s younger
         // ones are outstanding (they complete in issue order)
         int nvm = 0;
-        load_tab(0, tn);
+        load_tab(ch_lo, tn);
         nvm += 5;
         stage_tab(tn, 0);
         mc = tn.m;
         unsigned long long pred_c = 0, pred_n = 0;
         uint32_t start_c = ab;                     // assumed start of chunk ch's prediction
-        uint32_t end_c = predict(0, 0, mc, ab, pred_c);  // and its predicted end
+        uint32_t end_c = predict(ch_lo, 0, mc, ab, pred_c);  // and its predicted end
         if (!staged) pred_c = 0;
         // predicted blocks of chunk ch not fetched yet, how many are issued, and the stamp of
         // its first NS fetches; lane k of `stamp`: nvm after the fetch of predicted block #k
-        unsigned long long rem_c = issue_slots(0, pred_c, 0, nvm), rem_n = 0;
+        unsigned long long rem_c = issue_slots(ch_lo, pred_c, 0, nvm), rem_n = 0;
         int iss_c = min(__builtin_popcountll(pred_c), NS), iss_n = 0;
         int stamp_c = nvm, stamp_n = 0;
         int stamp = 0;
-        if (nch > 1) {
-            load_tab(1, tn);
+        if (nch > ch_lo + 1) {
+            load_tab(ch_lo + 1, tn);
             nvm += 5;
             stage_tab(tn, 1);
             mn = tn.m;
         }
-        if (nch > 2) {  // in flight during chunk 0
-            load_tab(2, tn);
+        if (nch > ch_lo + 2) {  // in flight during the first chunk
+            load_tab(ch_lo + 2, tn);
             nvm += 5;
         }
         PH_MARK(0);
-        for (int ch = 0; ch < nch; ++ch) {
-            const int buf = ch & 1;
+        for (int ch = ch_lo; ch < nch; ++ch) {
+            const int buf = (ch - ch_lo) & 1;
             const int nb = chunk_nb(ch);
+            const int buf_off = buf ? set_off : 0;
             // prediction of chunk ch + 1 (its start: chunk ch's predicted end, moved by the
             // error of chunk ch's assumed start) and its first slot fetches, in flight during ch
             uint32_t start_n = 0, end_n = 0;
@@ -802,11 +826,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
             PH_MARK(1);
             PH_COUNT(8, 1);
             PH_COUNT(9, __builtin_popcountll(pred_c));
-#ifdef LGCN_WALK_FINE_WAIT
-            wait_vm_upto(nvm - stamp_c);  // chunk ch's first slots have landed
-#else
             wait_vm_coarse(nvm - stamp_c);  // chunk ch's first slots have landed
-#endif
             PH_MARK(2);
             int from = 0;
             bool direct = false;  // block `from` is re-run without a test (a predicted run)
@@ -830,7 +850,8 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                 // predicted ones (at most NS ahead of f, so f's own slot is kept)
                 const int done = __builtin_popcountll(pred_c & ((1ull << f) - 1ull));
                 while (rem_c && iss_c < done + NS) {
-                    fetch(fb + 1 + (int64_t)ch * CH + __builtin_ctzll(rem_c), buf * NS + iss_c % NS);
+                    fetch(1 + ch * CH + __builtin_ctzll(rem_c),
+                          buf_off + __builtin_amdgcn_readlane(ring, iss_c));
                     nvm += 2;
                     stamp = lane == iss_c ? nvm : stamp;
                     rem_c &= rem_c - 1;
@@ -843,19 +864,15 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
 #ifdef LGCN_EMU_STATS
                 const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-                int sl;
+                int sl;  // the block's slot: float offset from s_dyn
                 if ((pred_c >> f) & 1ull) {
-                    sl = buf * NS + done % NS;
+                    sl = buf_off + __builtin_amdgcn_readlane(ring, done);
                     if (done >= NS) {  // a refill: wait for its own fetch only
-#ifdef LGCN_WALK_FINE_WAIT
-                        wait_vm_upto(nvm - __builtin_amdgcn_readlane(stamp, done));
-#else
                         wait_vm_coarse(nvm - __builtin_amdgcn_readlane(stamp, done));
-#endif
                         PH_MARK(5);
                     }
                 } else {  // not predicted: fetched now into the spare slot
-                    sl = spare;
+                    sl = spare * 2 * B;
                     EMU_STAT(3, 1);
                     PH_COUNT(11, 1);
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
@@ -863,7 +880,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                     } else
 #endif
                     if (staged) {
-                        fetch(fb + kb, sl);
+                        fetch(kb, sl);
                         nvm += 2;
                         // the youngest operation: everything older lands before it anyway
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -878,9 +895,9 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                             vq[k] = j < n ? __int_as_float(r.y) : 0.f;
                             xq[k] = load_elem<XD>(x, x_nz, r.x, c, xdiv, j < n);
                         }
-                        *reinterpret_cast<float4*>(slot_v(sl) + 4 * lane) =
+                        *reinterpret_cast<float4*>(s_dyn + sl + 4 * lane) =
                             make_float4(vq[0], vq[1], vq[2], vq[3]);
-                        *reinterpret_cast<float4*>(slot_x(sl) + 4 * lane) =
+                        *reinterpret_cast<float4*>(s_dyn + sl + B + 4 * lane) =
                             make_float4(xq[0], xq[1], xq[2], xq[3]);
                     }
                     PH_MARK(5);
@@ -888,7 +905,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
                 if (g_emu_mode != 1 && g_emu_mode < 4)
 #endif
-                    ab = resolve_block(slot_v(sl), slot_x(sl), n, ab, max_it, iters);
+                    ab = resolve_block(s_dyn + sl, s_dyn + sl + B, n, ab, max_it, iters);
                 PH_MARK(4);
                 PH_COUNT(10, 1);
 #ifdef LGCN_EMU_STATS
@@ -943,6 +960,10 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     }
 #endif
     if (lane != 0) return;
+    if (nch < nch_all) {  // chunks left for a later window: carry the chain value there
+        *carry = (int)ab;
+        return;
+    }
     const int32_t row = er.row;
     float out = __uint_as_float(ab);
     if constexpr (MODE == LGCN_EPI_MEAN) {
@@ -967,22 +988,25 @@ bool is_pow2(float x) {
     return x > 0.f && frexpf(x, &e) == 0.5f;
 }
 
+// n_blocks blocks from `blocks`; or (prows) blocks [k_lo, k_hi) of rows prows[0 .. n_blocks)
 template <int XD>
 int launch_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                   const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, int4* ktab,
-                  int4* meta, float* stage, const lgcn_emu_row_t* live, hipStream_t s) {
-    const dim3 grid((uint32_t)n_blocks, (uint32_t)((d + 63) / 64));
+                  int4* meta, float* stage, const lgcn_emu_row_t* live, hipStream_t s,
+                  const lgcn_emu_row_t* prows = nullptr, int32_t k_lo = 0, int32_t k_hi = 0) {
+    const dim3 grid(prows ? (uint32_t)(k_hi - k_lo) : (uint32_t)n_blocks, (uint32_t)((d + 63) / 64),
+                    prows ? (uint32_t)n_blocks : 1u);
     hipLaunchKernelGGL((k_emu_blocks<XD>), grid, dim3(64), 0, s, edges, blocks, x, xdiv, x_nz, d,
-                       ktab, meta, stage, live);
+                       ktab, meta, stage, live, prows, k_lo, k_hi);
     return herr_x(hipGetLastError());
 }
 
 template <int MODE, int XD>
 int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
+                const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, int4* meta,
                 const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
                 int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
-                const lgcn_emu_row_t* live, hipStream_t s) {
+                const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi, hipStream_t s) {
     const dim3 grid((uint32_t)n_rows, (uint32_t)d);
     const size_t lds = (size_t)(2 * slots + 1) * 2 * LGCN_EMU_BLOCK * sizeof(float);
     if (lds > 56 * 1024) {
@@ -993,16 +1017,26 @@ int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         if (hipError_t e = hipGetDevice(&dev)) return (int)e;
         const uint64_t bit = dev < 64 ? (1ull << dev) : 0;
         if (!bit || !(raised.load(std::memory_order_relaxed) & bit)) {
-            const hipError_t e = hipFuncSetAttribute(
-                reinterpret_cast<const void*>(&k_emu_walk<MODE, XD>),
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
-            if (e != hipSuccess) return (int)e;
+            for (const void* f : {reinterpret_cast<const void*>(&k_emu_walk<MODE, XD, false>),
+                                  reinterpret_cast<const void*>(&k_emu_walk<MODE, XD, true>)}) {
+                const hipError_t e = hipFuncSetAttribute(
+                    f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
+                if (e != hipSuccess) return (int)e;
+            }
             raised.fetch_or(bit, std::memory_order_relaxed);
         }
     }
-    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, ktab,
-                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots, lgcn_detail::g_emu_resolve,
-                       live);
+#ifndef LGCN_WALK_ISO_SLOTS
+#define LGCN_WALK_ISO_SLOTS 1000  // (build-time A/B: walks of this many slots or more isolated)
+#endif
+    if (slots >= LGCN_WALK_ISO_SLOTS)
+        hipLaunchKernelGGL((k_emu_walk<MODE, XD, true>), grid, dim3(64), lds, s, edges, blocks,
+                           rows, ktab, meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
+                           lgcn_detail::g_emu_resolve, live, ch_lo, ch_hi);
+    else
+        hipLaunchKernelGGL((k_emu_walk<MODE, XD, false>), grid, dim3(64), lds, s, edges, blocks,
+                           rows, ktab, meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
+                           lgcn_detail::g_emu_resolve, live, ch_lo, ch_hi);
     return herr_x(hipGetLastError());
 }
 
@@ -1012,12 +1046,12 @@ int xd_of(float xdiv, const uint32_t* x_nz) {
 
 template <int MODE>
 int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-              const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
+              const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, int4* meta,
               const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
               int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
-              const lgcn_emu_row_t* live, hipStream_t s) {
+              const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi, hipStream_t s) {
 #define LGCN_W(XD_) \
-    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, live, s);
+    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
     switch (xd) {
         LGCN_W(0) LGCN_W(1) LGCN_W(2) LGCN_W(4) LGCN_W(5) LGCN_W(6)
         default: return LGCN_EINVAL;
@@ -1438,11 +1472,38 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
 #undef LGCN_B
 }
 
-int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                  const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
-                  const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
-                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
-                  const lgcn_emu_row_t* live, void* stream) {
+int lgcn_emu_blocks_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                         const lgcn_emu_row_t* rows, int32_t n_rows, int32_t k_lo, int32_t k_hi,
+                         lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
+                         void* meta, float* stage, const lgcn_emu_row_t* live, void* stream) {
+    if (n_rows < 0 || n_rows > 65535 || k_lo < 0 || d < 1 || d > 2048 || !(x_div > 0.f))
+        return LGCN_EINVAL;
+    if (n_rows == 0 || k_hi <= k_lo) return 0;
+    if (!edges || !blocks || !rows || !rel || !meta || !x.p0) return LGCN_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(rel) & 15) || (reinterpret_cast<uintptr_t>(meta) & 15) ||
+        (reinterpret_cast<uintptr_t>(stage) & 15))
+        return LGCN_EALIGN;
+    const int xd = xd_of(x_div, x_nz);
+    const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int4* mp = static_cast<int4*>(meta);
+    int4* kp = reinterpret_cast<int4*>(rel);
+#define LGCN_B(XD_) \
+    case XD_: return launch_blocks<XD_>(edges, blocks, n_rows, x, xa, x_nz, d, kp, mp, stage, live, s, rows, k_lo, k_hi);
+    switch (xd) {
+        LGCN_B(0) LGCN_B(1) LGCN_B(2) LGCN_B(4) LGCN_B(5) LGCN_B(6)
+        default: return LGCN_EINVAL;
+    }
+#undef LGCN_B
+}
+
+int lgcn_emu_walk_chunks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                         const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, void* meta,
+                         const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz,
+                         float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                         int32_t slots, const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi,
+                         void* stream) {
+    if (ch_lo < 0 || ch_hi <= ch_lo) return LGCN_EINVAL;
     if (slots == 0) slots = LGCN_EMU_SLOTS;
     // static LDS (two translation tables, 8 KB) + (2 slots + 1) x 2 KB within 64 KB
     if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host || slots < 1 ||
@@ -1468,18 +1529,29 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     const int xd = xd_of(x_div, x_nz);
     const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int4* mp = static_cast<const int4*>(meta);
+    int4* mp = static_cast<int4*>(meta);
     const int4* kp = reinterpret_cast<const int4*>(rel);
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
+            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
         case LGCN_EPI_MEAN:
-            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
+            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
         case LGCN_EPI_ADD:
-            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
+            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
         default:
             return LGCN_EINVAL;
     }
+}
+
+int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                  const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
+                  const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
+                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
+                  const lgcn_emu_row_t* live, void* stream) {
+    // every chunk in one window: meta is only read
+    return lgcn_emu_walk_chunks(edges, blocks, rows, n_rows, rel, const_cast<void*>(meta), stage,
+                                x, x_div, x_nz, y, ldy, d, epi_host, slots, live, 0, INT32_MAX,
+                                stream);
 }
 
 

@@ -27,11 +27,12 @@ TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3,
 TUNE_EMU_RESOLVE = 5
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
-SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST = 7, 8, 9
+SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST, SCHED_MEAN_EARLY = 7, 8, 9, 10
+SCHED_PIECES, SCHED_CHAINS_FIRST = 11, 12
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
-ABI_VERSION = 11
+ABI_VERSION = 12
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -116,7 +117,8 @@ class PlanT(ctypes.Structure):
                 ("n_rows", ctypes.c_int32), ("n_pre", ctypes.c_int32),
                 ("n_emu_blocks", ctypes.c_int32), ("n_emu_rows", ctypes.c_int32),
                 ("emu_part_rows", ctypes.c_int32 * 2), ("emu_part_blocks", ctypes.c_int32 * 2),
-                ("emu_scratch_blocks", ctypes.c_int32), ("emu_live", ctypes.c_void_p)]
+                ("emu_scratch_blocks", ctypes.c_int32), ("emu_live", ctypes.c_void_p),
+                ("emu_part_max_blocks", ctypes.c_int32 * 2)]
 
 
 class LgcnError(RuntimeError):
@@ -167,6 +169,11 @@ ABI = [
                                        _P, _P]),
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
                                      _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P, _P]),
+    ("lgcn_emu_blocks_rows", ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, RowsT, ctypes.c_float,
+                                            _P, _I32, _P, _P, _P, _P, _P]),
+    ("lgcn_emu_walk_chunks", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float,
+                                            _P, _P, _I64, _I32, ctypes.POINTER(EpilogueT), _I32,
+                                            _P, _I32, _I32, _P]),
     ("lgcn_chain_supported", ctypes.c_int, [_I32]),
     ("lgcn_live_scratch_bytes", ctypes.c_size_t, [_I32, _I32]),
     ("lgcn_live_rows", ctypes.c_int, [_P, _P, _I32, _P, _I32, RowsT, ctypes.c_float, _P, _P, _I64,
@@ -443,6 +450,10 @@ class HubPlan:
         p.emu_part_rows[0], p.emu_part_rows[1] = rows
         p.emu_part_blocks[0], p.emu_part_blocks[1] = blocks
         p.emu_scratch_blocks = need
+        # the longest row of each walked part (emu_nb: longest first)
+        nb = self.emu_nb
+        p.emu_part_max_blocks[0] = int(nb[0]) if rows[0] > 0 else 0
+        p.emu_part_max_blocks[1] = int(nb[rows[0]]) if rows[1] > rows[0] else 0
         lv = self.live_scratch(device) if live and self.mode == "exact" else None
         p.emu_live = lv.data_ptr() if lv is not None else None
         return p
@@ -915,6 +926,16 @@ class Sched:
         # before the layer kernel fills the chip (C3 forward 18.58 -> 18.06 ms; LGCN_BLOCKS_FIRST=0
         # starts them together)
         self.set(SCHED_BLOCKS_FIRST, 0 if os.environ.get("LGCN_BLOCKS_FIRST", "1") == "0" else 1)
+        # the final half-layer of a side forks its block passes before waiting for the other
+        # lane's layer K-1 (they read X only; LGCN_MEAN_EARLY=0: the whole half-layer waits)
+        self.set(SCHED_MEAN_EARLY, 0 if os.environ.get("LGCN_MEAN_EARLY", "1") == "0" else 1)
+        # LGCN_PIECES=2..4: parts 0 and 1 pipeline block pass and walk in chunk windows (A/B at
+        # C3: 14.23 vs 14.07 ms whole — the walk's first chunks are its slowest, and the
+        # windows' block passes share its SIMDs)
+        self.set(SCHED_PIECES, sched_pieces())
+        # LGCN_CHAINS_FIRST=1: a half-layer without walks (C3's users) runs its chain rows before
+        # its layer kernel (A/B: 13.7 ms best case at C3 but bimodal under the lane priorities)
+        self.set(SCHED_CHAINS_FIRST, 1 if os.environ.get("LGCN_CHAINS_FIRST", "0") == "1" else 0)
 
     def set(self, knob, value):
         _check(self.lib.lgcn_sched_set(self.handle, knob, int(value)), "lgcn_sched_set")
@@ -928,13 +949,14 @@ class Sched:
 
 
 def _capture_aux(device):
-    """Auxiliary streams while the caller's stream is being captured into a HIP graph: at most 3
-    (one lane). The two-lane schedule's 8 streams forked and joined inside one capture crash
-    hipStreamEndCapture on this ROCm (segfault, tests/test_gpu_sides.py), so a captured sided
-    propagation runs its half-layers in order on one lane — same kernels, same bits."""
+    """Auxiliary streams while the caller's stream is being captured into a HIP graph: the same
+    as eager (LGCN_CAPTURE_AUX overrides, for A/B). The C library keeps a capture safe itself:
+    under a capture lane 1 runs its half-layers on its main stream alone (lgcn_engine.hip
+    make_lanes — forking lane 1's own aux streams inside a capture crashes hipStreamEndCapture
+    on this ROCm), so a captured sided propagation still runs two lanes, same kernels and bits."""
     if torch.cuda.is_current_stream_capturing():
         cap = os.environ.get("LGCN_CAPTURE_AUX", "")
-        return min(int(cap) if cap else 3, n_aux_streams())
+        return min(int(cap), n_aux_streams()) if cap else n_aux_streams()
     return None
 
 
@@ -944,12 +966,21 @@ def sched_for(device, n_aux=None):
     if not emu_overlap_enabled():
         return None
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_BLOCKS_FIRST", ""))
+           os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_BLOCKS_FIRST", ""),
+           os.environ.get("LGCN_MEAN_EARLY", ""), os.environ.get("LGCN_PIECES", ""),
+           os.environ.get("LGCN_CHAINS_FIRST", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
         if key[1] > 3:  # the one-lane schedule a capture falls back to, made outside any capture
             sched_for(device, 3)
     return _scheds[key]
+
+
+def sched_pieces():
+    """Chunk windows of the pipelined block pass + walk of parts 0 and 1 (LGCN_PIECES, 0..4;
+    0/1 = each part's block pass, then its walk)."""
+    v = os.environ.get("LGCN_PIECES", "0")
+    return max(0, min(4, int(v))) if v.strip() else 0
 
 
 def chain_enabled():
@@ -1096,7 +1127,9 @@ last_schedule = None  # the schedule of the latest propagation call (diagnostics
 def _note_schedule(sc, sided):
     global last_schedule
     n = sc.n_aux if sc is not None else 0
-    last_schedule = {"sided": sided, "aux_streams": n, "lanes": 2 if sided and n >= 4 else 1}
+    # captured: lane 1 runs on its main stream alone (the C library's capture rule, make_lanes)
+    last_schedule = {"sided": sided, "aux_streams": n, "lanes": 2 if sided and n >= 4 else 1,
+                     "captured": torch.cuda.is_current_stream_capturing()}
 
 
 def use_sides(graph, layer_events=None, kernel_events=None):

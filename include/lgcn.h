@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 11
+#define LGCN_ABI_VERSION 12
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -165,6 +165,10 @@ typedef struct {
      * 256-B aligned: with a row-sparse X (x_nz) every emulated row runs as a chain over its live
      * edges (lgcn_live_rows) instead of block pass + walk / chain over all of them */
     void* emu_live;
+    /* the longest row's block count in part 0 / part 1 (lgcn_plan_exact writes them); with
+     * LGCN_SCHED_PIECES the layer pipelines a part's block pass and walk in chunk windows up to
+     * it. 0 = unknown: that part runs whole */
+    int32_t emu_part_max_blocks[2];
 } lgcn_hub_plan_t;
 
 /* Host planner of an exact hub plan (host memory only, no GPU call): from the host row pointers
@@ -174,8 +178,8 @@ typedef struct {
  * [n_emu_blocks] (copy both to the device for plan->emu_rows / emu_blocks). Part 0 = rows of
  * more than max(part0_blocks, ceil(chain_max / LGCN_EMU_BLOCK)) blocks, part 1 = rows of more
  * than ceil(chain_max / LGCN_EMU_BLOCK), the rest run as sequential chains (lgcn_chain_rows).
- * Writes plan->n_emu_rows, n_emu_blocks, emu_part_rows, emu_part_blocks and emu_scratch_blocks
- * (= emu_part_blocks[1]); nothing else. Two-call protocol: rows_host = blocks_host = NULL writes
+ * Writes plan->n_emu_rows, n_emu_blocks, emu_part_rows, emu_part_blocks, emu_part_max_blocks and
+ * emu_scratch_blocks (= emu_part_blocks[1]); nothing else. Two-call protocol: rows_host = blocks_host = NULL writes
  * only the counts. chain_max <= 0: lgcn_chain_max_default(nnz); part0_blocks <= 0: 8192.
  * emu_min_degree = the bundle threshold (128) for the default exact plan. Replaces, for a C
  * host, the Python planner engine.plan_hubs (which calls it). */
@@ -373,6 +377,28 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
                   const lgcn_emu_row_t* live, void* stream);
 
+/* The block pass and the walk in chunk windows, so a walk can start before the whole block pass
+ * is done (lgcn_layer pipelines them this way, LGCN_SCHED_PIECES). A row's block k > 0 lies in
+ * chunk (k - 1) / 64 (block 0 starts the chain).
+ * lgcn_emu_blocks_rows: the block pass of blocks [k_lo, k_hi) of each of rows[0 .. n_rows)
+ * (n_rows <= 65535; blocks / rel / meta / stage indexed by the rows' first_block, the whole
+ * arrays as for lgcn_emu_walk).
+ * lgcn_emu_walk_chunks: lgcn_emu_walk over chunks [ch_lo, ch_hi) of every row. The first
+ * window (ch_lo = 0) starts from block 0's chain; a row with chunks past ch_hi leaves its chain
+ * value in block 0's meta record (so meta is written) for the next window, which starts from it;
+ * the window holding a row's last chunk writes its Y row. Windows of one row run in order, each
+ * after the block pass of its chunks (and block 0 before the first). */
+int lgcn_emu_blocks_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                         const lgcn_emu_row_t* rows, int32_t n_rows, int32_t k_lo, int32_t k_hi,
+                         lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
+                         void* meta, float* stage, const lgcn_emu_row_t* live, void* stream);
+int lgcn_emu_walk_chunks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                         const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, void* meta,
+                         const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz,
+                         float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                         int32_t slots, const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi,
+                         void* stream);
+
 /* Mid-size emulated rows run as the reference's sequential chain itself (no block pass): one
  * wave per (row, column slice) folds acc = fma(val_j, X[col_j, c], acc) in stored order from +0
  * while the next windows of gathered X rows are in flight by LDS-DMA. rows / blocks: as for
@@ -415,10 +441,10 @@ const lgcn_emu_row_t* lgcn_live_flags(const void* scratch, int32_t n_rows, int32
  * Bipartite lanes (lgcn_propagate_*_sides): with n_aux = 4 + m (m = 0..3), aux_streams[3] is
  * the main stream of the second lane of half-layers and [4..3+m] its part 0 / part 1 / chain
  * streams ([4] high priority), so the two chains of half-layers run side by side; with n_aux <= 3
- * both lanes share the caller's stream and [0..2]. Every stream, the caller's included, wants a
- * hardware queue of its own: 8 streams need GPU_MAX_HW_QUEUES >= 8 in the environment before
- * the process first touches the GPU (HIP's default is 4; with fewer queues streams share them
- * and the lanes partly serialise — same results).
+ * both lanes share the caller's stream and [0..2]. HIP keeps a pool of hardware queues per
+ * stream priority (GPU_MAX_HW_QUEUES each, default 4): with lane 1's four streams created at
+ * high priority and the caller's + aux 0..2 at normal priority, every stream has a queue of its
+ * own under the default (measured at C3: as fast as GPU_MAX_HW_QUEUES=8).
  * lgcn_sched_create allocates the events (the only allocating call; once per stream set); NULL
  * sched = everything in order on the caller's stream. */
 typedef struct lgcn_sched lgcn_sched_t;
@@ -442,6 +468,22 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        longest rows' walk then starts before the layer kernel
                                        fills the chip; engine.py sets it); 0 (the C default):
                                        they start together */
+#define LGCN_SCHED_MEAN_EARLY   10  /* 1: lgcn_propagate_forward_sides' final (mean) half-layer of a
+                                       side forks its block passes before it waits for that side's
+                                       layer K-1 on the other lane (they read X only); its layer
+                                       kernel, walks and chains wait (engine.py sets it); 0 (the
+                                       C default): the whole half-layer waits */
+#define LGCN_SCHED_PIECES       11  /* 2..4: parts 0 and 1 pipeline their block pass and walk in
+                                       that many chunk windows (0-3, 4-15, 16-63, 64+ chunks; the
+                                       last open): the block pass windows run on the caller's
+                                       stream before the layer kernel, the walk of a window starts
+                                       once its own block pass is done (lgcn_emu_blocks_rows /
+                                       lgcn_emu_walk_chunks; needs the plan's
+                                       emu_part_max_blocks). 0, 1 (the C default): whole parts */
+#define LGCN_SCHED_CHAINS_FIRST 12  /* 1: a layer that walks no rows (parts 0 and 1 empty) runs its
+                                       chain rows on the caller's stream before the layer kernel
+                                       (beside it on an aux stream they are dispatched only once
+                                       the layer kernel's grid is); 0 (the C default): beside */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 11
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 12
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -107,7 +107,17 @@ def test_argument_validation_without_gpu(lib):
                                None) == 0     # nothing to do
     assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 12, ctypes.byref(ep),
                                None) == -1    # unsupported width
-    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8  # (+ padding, emu_live)
+    # (+ padding, emu_live, emu_part_max_blocks)
+    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8 + 8
+    # chunk windows: a window must be non-empty; row windows of at most 65535 rows
+    assert lib.lgcn_emu_walk_chunks(None, None, None, 2, None, None, None, rows, 1.0, None, None,
+                                    64, 64, ctypes.byref(ep), 8, None, 4, 4, None) == -1
+    assert lib.lgcn_emu_walk_chunks(None, None, None, 2, None, None, None, rows, 1.0, None, None,
+                                    64, 64, ctypes.byref(ep), 8, None, -1, 4, None) == -1
+    assert lib.lgcn_emu_blocks_rows(None, None, None, 70000, 0, 4, rows, 1.0, None, 64, None,
+                                    None, None, None, None) == -1
+    assert lib.lgcn_emu_blocks_rows(None, None, None, 2, 4, 4, rows, 1.0, None, 64, None, None,
+                                    None, None, None) == 0   # empty window: nothing to do
     # live-edge rows: the row mask and the scratch are required, widths as the chain kernel's
     assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, None, None, 64, 64,
                               ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # no x_nz

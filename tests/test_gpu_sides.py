@@ -82,7 +82,8 @@ def test_sides_bitwise(gpu_device, monkeypatch, brand_graph, n_aux, kind):
 
 def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):
     """The model's entry (propagate_blocks: sides from the segment sizes) forward + autograd
-    backward, and the forward captured in a HIP graph (8 streams forked and joined)."""
+    backward, and the forward captured in a HIP graph on the two lanes (the caller's stream, its
+    3 aux streams and lane 1's main stream forked and joined)."""
     monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
     monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
     r, c, v, n = brand_graph
@@ -102,6 +103,8 @@ def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):
     assert np.array_equal(got_b, oracle.backward(r, c, v, G, 3))
     x = [t.detach() for t in w]
     cap = engine.CapturedForward(g, x, 3, hub_threshold=128)
+    # the capture ran the two lanes (lane 1 without its own aux streams: make_lanes' rule)
+    assert engine.last_schedule == {"sided": True, "aux_streams": 7, "lanes": 2, "captured": True}
     for _ in range(2):
         assert np.array_equal(cap.replay().cpu().numpy(), want)
 
@@ -173,6 +176,7 @@ def test_default_environment_runs_two_lanes(gpu_device, monkeypatch, brand_graph
     e0 = _e0(np.random.default_rng(12), "xavier", n, 64)
     w = _segs(e0, gpu_device)
     out = engine.propagate_blocks(adj, w, 3, hub_threshold=128)
-    assert engine.last_schedule == {"sided": True, "aux_streams": 7, "lanes": 2}
+    assert engine.last_schedule == {"sided": True, "aux_streams": 7, "lanes": 2,
+                                    "captured": False}
     got = torch.cat([o.detach() for o in out]).cpu().numpy()
     assert np.array_equal(got, oracle.forward(r, c, v, e0, 3))

@@ -143,6 +143,9 @@ def test_c_planner_parts_and_scratch():
     assert list(plan.emu_part_rows) == [sum(x > 8192 for x in nb), sum(x > b1 for x in nb)]
     assert plan.emu_part_blocks[0] == sum(x for x in nb if x > 8192)
     assert plan.emu_part_blocks[1] == plan.emu_scratch_blocks == sum(x for x in nb if x > b1)
+    # the longest row of each walked part (the pieced schedule's chunk windows reach it)
+    assert list(plan.emu_part_max_blocks) == [max(x for x in nb if x > 8192),
+                                              max(x for x in nb if b1 < x <= 8192)]
     rows = np.empty((plan.n_emu_rows, 4), np.int32)
     blocks = np.empty((plan.n_emu_blocks, 4), np.int32)
     assert lib.lgcn_plan_exact(rowptr.ctypes.data, None, deg.size, 128, 60_000, 8192,
@@ -151,6 +154,8 @@ def test_c_planner_parts_and_scratch():
     hp = engine.HubPlan(128, emu_nb=np.array(nb))
     pr, pb = hp.walk_parts(60_000 * 1024)  # chain_max_degree(nnz) = 60_000 ... clamped to 65536
     assert pr[0] == plan.emu_part_rows[0]
+    assert hp.struct(64, "cpu", nnz=60_000 * 1024).emu_part_max_blocks[0] == \
+        plan.emu_part_max_blocks[0]
     sizes = (ctypes.c_size_t * 3)()
     assert lib.lgcn_plan_scratch_bytes(ctypes.byref(plan), 64, 0, sizes) == 0
     nbw = plan.emu_part_blocks[1]

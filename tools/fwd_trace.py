@@ -54,8 +54,8 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(a.elapsed_time(b))
             print(f"{name}: median {np.median(ts):.3f} ms min {min(ts):.3f} "
-                  f"[{os.environ.get('LGCN_LIB', 'product')} slots={os.environ.get('LGCN_EMU_SLOTS', '')}]",
-                  flush=True)
+                  f"[{os.environ.get('LGCN_LIB', 'product')} slots={os.environ.get('LGCN_EMU_SLOTS', '')}]"
+                  f" all {' '.join(f'{t:.2f}' for t in ts)}", flush=True)
         return
     for _, fn in runs:
         for _ in range(3):
