@@ -662,7 +662,7 @@ def main():
                    "interactions": cfg["interactions"], "nnz": nnz, "d": d, "layers": K,
                    "brands": B, "content_dim": fusion,
                    "hub_threshold": hub_thr, "hub_mode": hub_mode,
-                   "emu_min_degree": engine.emu_min_degree_from_env(),
+                   "emu_min_degree": engine.emu_min_degree_from_env(nnz),
                    "schedule": ("bipartite two-lane (lgcn_propagate_forward_sides), "
                                 f"{engine.n_aux_streams()} aux streams, GPU_MAX_HW_QUEUES="
                                 f"{os.environ.get('GPU_MAX_HW_QUEUES', 'unset (HIP default 4)')}") if sided else "one operator",

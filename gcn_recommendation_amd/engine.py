@@ -46,10 +46,15 @@ LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 DEFAULT_HUB_THRESHOLD = 128
 HUB_MODES = ("exact", "chunk")
 # Rows above the bundle threshold and up to this degree run inside the layer kernel as one lane
-# group's chain each (LGCN_EMU_MIN_DEGREE); 0 (default) = none: every row above the threshold
-# goes to the emulated-row list, where the shorter ones run as sequential chains of their own
+# group's chain each (LGCN_EMU_MIN_DEGREE; hub items dispatched first in its grid); longer rows go
+# to the emulated-row list, where the shorter ones run as sequential chains of their own
 # (lgcn_chain_rows, beside the layer kernel) and the longest are block-emulated (emu_parts).
+# Default by graph size: 0 (none) below 2^23 nonzeros, 1024 above — at C3 the
+# rows of 129..1024 edges (most of the ~12k chain rows) were a chain kernel whose grid waited
+# behind the layer kernel's on a shared dispatch pipe; inside the layer kernel: forward 14.0-14.4
+# -> 12.6-13.0 ms (sweep 512 / 1024 / 1536 / 2048: 12.9-13.0 / 12.6-13.0 / 12.7-13.1 / 12.7-13.3)
 DEFAULT_EMU_MIN_DEGREE = 0
+DEFAULT_EMU_MIN_DEGREE_LARGE = 1024
 
 
 def hub_mode_from_env():
@@ -65,9 +70,13 @@ def emu_stage_enabled():
     return os.environ.get("LGCN_EMU_STAGE", "1") != "0"
 
 
-def emu_min_degree_from_env():
+def emu_min_degree_from_env(nnz=None):
+    """LGCN_EMU_MIN_DEGREE, else the default for a graph of nnz nonzeros (None: small)."""
     v = os.environ.get("LGCN_EMU_MIN_DEGREE", "")
-    return int(v) if v else DEFAULT_EMU_MIN_DEGREE
+    if v:
+        return int(v)
+    return DEFAULT_EMU_MIN_DEGREE_LARGE if nnz is not None and nnz >= (1 << 23) \
+        else DEFAULT_EMU_MIN_DEGREE
 
 
 def chain_max_degree(nnz):
@@ -578,7 +587,7 @@ class Graph:
         mode = mode or hub_mode_from_env()
         if mode not in HUB_MODES:
             raise LgcnError(f"unknown hub mode {mode!r}")
-        emu_min = emu_min_degree_from_env() if emu_min is None else emu_min
+        emu_min = emu_min_degree_from_env(self.nnz) if emu_min is None else emu_min
         chunk = chunk or hub_chunk_for(self.nnz)
         key = (threshold, mode) + ((chunk, DEFAULT_HUB_PRE_GROUP) if mode == "chunk" else (emu_min,))
         if key not in self._plans:
@@ -595,7 +604,7 @@ class Graph:
         mode = mode or hub_mode_from_env()
         if mode not in HUB_MODES:
             raise LgcnError(f"unknown hub mode {mode!r}")
-        emu_min = emu_min_degree_from_env() if emu_min is None else emu_min
+        emu_min = emu_min_degree_from_env(self.nnz) if emu_min is None else emu_min
         chunk = chunk or hub_chunk_for(self.nnz)
         key = ("sides", threshold, mode) + \
             ((chunk, DEFAULT_HUB_PRE_GROUP) if mode == "chunk" else (emu_min,))
