@@ -428,10 +428,12 @@ const char* lgcn_error_string(int code) {
 }
 
 int32_t lgcn_chain_max_default(int64_t nnz) {
-    // a chain row must stay short against a whole layer (C3: 56M nonzeros, ~3 ms per layer ->
-    // 55k edges); on a small graph the floor: a walk's fixed costs (block pass + walk ~0.4 ms per
-    // layer at C2) outweigh a 8k-edge chain (C2: 2048 -> 8192: forward 1.10 -> 0.94 ms)
-    return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 1024, 8192), 65536);
+    // a chain row must stay short against a whole layer (C3: 56M nonzeros, ~4 ms per layer ->
+    // 110k edges: forward 13.4 -> 13.2 ms and BPR backward 9.7 -> 9.4 ms against 55k; 220k:
+    // forward 12.8 ms but backward 10.2 ms); on a small graph the floor: a walk's fixed costs
+    // (block pass + walk ~0.4 ms per layer at C2) outweigh a 8k-edge chain (C2: 2048 -> 8192:
+    // forward 1.10 -> 0.94 ms)
+    return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 512, 8192), 131072);
 }
 
 int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,

@@ -1082,8 +1082,10 @@ struct ChainCfg {
     // X windows in flight while one is folded: as many as vmcnt (<= 63 outstanding) allows
     // with NI + 2 loads per window (W=64: 3 x 18, W=32: 6 x 10, W=16: 8 x 6)
     static constexpr int AHEAD = W == 64 ? 3 : W == 32 ? LGCN_CHAIN_AHEAD32 : 8;
-    static constexpr int NX = AHEAD + 1;    // X windows in the ring
-    static constexpr int NR = 2 * AHEAD + 1;  // record windows in the ring
+    // rings: X windows (>= AHEAD + 1), record windows (>= 2 AHEAD + 1); at W = 32 powers of two
+    // (8 and 16: the ring index is a mask, not a division; 72 KB of LDS, still 2 waves per CU)
+    static constexpr int NX = W == 32 && AHEAD <= 7 ? 8 : AHEAD + 1;
+    static constexpr int NR = W == 32 && AHEAD <= 7 ? 16 : 2 * AHEAD + 1;
 };
 
 // 4 bytes per lane by LDS-DMA: lane l's dword at gsrc -> LDS byte address dst + 4 l (dst
@@ -1152,11 +1154,12 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     // Pipeline (A = AHEAD): iteration v issues x(v + A) then rec(v + 2A); the prologue runs
     // v = -A .. -1 after rec(0 .. A-1) have landed. At iteration w, x(w) and rec(w + A) (both
     // issued by iteration w - A) must have landed: A - 1 later iterations of NI + 2 loads each
-    // may still be in flight. Ring slots: x(w + A) reuses window w - 1's slot (NX = A + 1),
-    // rec(w + 2A) record window w - 1's (NR = 2A + 1). The LDS-DMA is hidden from the compiler
+    // may still be in flight. Ring slots: x(w + A) takes a slot no window in [w, w + A) holds
+    // (NX >= A + 1), rec(w + 2A) one no record window in [w, w + 2A) holds (NR >= 2A + 1); with
+    // the minimum sizes that is window w - 1's. The LDS-DMA is hidden from the compiler
     // (dma4 / dma16): its LDS reads are then ordinary, scheduled and counted by it, and the
     // explicit vmcnt waits (asm, "memory") keep them behind the data they read.
-    static_assert(NX == AHEAD + 1 && NR == 2 * AHEAD + 1, "ring sizes");
+    static_assert(NX >= AHEAD + 1 && NR >= 2 * AHEAD + 1, "ring sizes");
     float acc = 0.f;
     if (nwin > 0) {  // (an empty row — live-edge rows may have none — reads no record)
     for (int w = 0; w < AHEAD; ++w) rec_dma(w);
