@@ -202,11 +202,27 @@ def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
     e.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(e) / args.train_steps
+    # the same loop with torch's fused Adam (one kernel per parameter instead of main.py's
+    # default foreach Adam, ~16 ms of multi_tensor_apply launches at C3): what the step costs
+    # when the optimizer is not the bottleneck
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    for b in batches[:2]:
+        step(b)
+    torch.cuda.synchronize()
+    a.record()
+    for b in batches[2:]:
+        step(b)
+    e.record()
+    torch.cuda.synchronize()
+    ms_fused = a.elapsed_time(e) / args.train_steps
     nnz = adj._nnz()
     out = {"ms_per_step": round(ms, 3), "propagated_edges_per_s": round(2 * K * nnz / (ms / 1e3), 1),
-           "batch": 2048, "optimizer": "Adam(lr=1e-3)", "loss_last": float(loss.item()),
+           "batch": 2048, "optimizer": "Adam(lr=1e-3) (main.py's default: foreach)",
+           "loss_last": float(loss.item()),
+           "fused_adam_ms_per_step": round(ms_fused, 3),
            "what": f"main.py:488-531 hot loop: forward + gathers + bpr_loss_reg + backward + "
-                   f"Adam over all {U + I:,} x {d} parameters"}
+                   f"Adam over all {U + I:,} x {d} parameters; fused_adam_ms_per_step: the same "
+                   f"with torch.optim.Adam(fused=True)"}
     del model, opt
     torch.cuda.empty_cache()
     return out

@@ -822,6 +822,7 @@ struct lgcn_sched {
     int pieces;
     hipEvent_t piece_ev[2][LGCN_SCHED_MAX_PIECES];
     int chains_first;  // LGCN_SCHED_CHAINS_FIRST
+    int lane_flip;     // LGCN_SCHED_LANE_FLIP: forward half-layer (k, side) on lane (k+side+K+1)%2
 };
 
 namespace {
@@ -1283,6 +1284,9 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
         case LGCN_SCHED_MEAN_EARLY:
             sc->mean_early = value != 0;
             return 0;
+        case LGCN_SCHED_LANE_FLIP:
+            sc->lane_flip = value != 0;
+            return 0;
         case LGCN_SCHED_CHAINS_FIRST:
             sc->chains_first = value != 0;
             if (sc->lane1) sc->lane1->chains_first = value != 0;
@@ -1390,7 +1394,7 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
         // the item side first: its half-layer holds the longest walks (host submission order
         // only; the two sides of one layer are independent)
         for (int side = 1; side >= 0; --side) {
-            const Lane& L = lanes[(k + side + K) & 1];
+            const Lane& L = lanes[(k + side + K + (sched && sched->lane_flip ? 1 : 0)) & 1];
             // the mean of a side reads its layer K-1, computed on the other lane: the half-layer
             // waits for it — or, with MEAN_EARLY, only its kernels that write Y do
             hipEvent_t late = nullptr;

@@ -28,7 +28,7 @@ TUNE_EMU_RESOLVE = 5
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
 SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST, SCHED_MEAN_EARLY = 7, 8, 9, 10
-SCHED_PIECES, SCHED_CHAINS_FIRST = 11, 12
+SCHED_PIECES, SCHED_CHAINS_FIRST, SCHED_LANE_FLIP = 11, 12, 13
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
@@ -945,6 +945,7 @@ class Sched:
         # LGCN_CHAINS_FIRST=1: a half-layer without walks (C3's users) runs its chain rows before
         # its layer kernel (A/B: 13.7 ms best case at C3 but bimodal under the lane priorities)
         self.set(SCHED_CHAINS_FIRST, 1 if os.environ.get("LGCN_CHAINS_FIRST", "0") == "1" else 0)
+        self.set(SCHED_LANE_FLIP, 1 if os.environ.get("LGCN_LANE_FLIP", "0") == "1" else 0)
 
     def set(self, knob, value):
         _check(self.lib.lgcn_sched_set(self.handle, knob, int(value)), "lgcn_sched_set")
@@ -977,7 +978,7 @@ def sched_for(device, n_aux=None):
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
            os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_BLOCKS_FIRST", ""),
            os.environ.get("LGCN_MEAN_EARLY", ""), os.environ.get("LGCN_PIECES", ""),
-           os.environ.get("LGCN_CHAINS_FIRST", ""))
+           os.environ.get("LGCN_CHAINS_FIRST", ""), os.environ.get("LGCN_LANE_FLIP", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
         if key[1] > 3:  # the one-lane schedule a capture falls back to, made outside any capture

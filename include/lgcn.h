@@ -484,6 +484,11 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        chain rows on the caller's stream before the layer kernel
                                        (beside it on an aux stream they are dispatched only once
                                        the layer kernel's grid is); 0 (the C default): beside */
+#define LGCN_SCHED_LANE_FLIP    13  /* 1: lgcn_propagate_forward_sides runs half-layer (k, side) on
+                                       lane (k + side + K + 1) % 2 — lane 1 (the high-priority
+                                       streams) then carries the chain ending in layer K's side 0
+                                       (users: the mean over the most rows, after the items' layer
+                                       K-1); 0 (the C default): (k + side + K) % 2 */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +
