@@ -361,6 +361,39 @@ int scale_rows(const lgcn_rows_t& x, int32_t n_rows, int32_t d, float div, float
     return dispatch_geo(g, f);
 }
 
+// S[row] = ((P0[row] + P1[row]) + ...) + P_{n-1}[row] (ep.prev0, ep.prev_dense: the first n_prev
+// terms of a MEAN epilogue, in its order) for the rows of slots [0, n_slots): a side's layer-K
+// mean then reads one row instead of n_prev (LGCN_SCHED_PRESUM). One float4 per thread.
+__global__ __launch_bounds__(256) void k_presum(const int32_t* __restrict__ row_ids,
+                                                int32_t n_slots, lgcn_epilogue_t ep, int32_t d,
+                                                float* __restrict__ S, int64_t lds) {
+    const int q = d >> 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = i / q;
+    if (slot >= n_slots) return;
+    const int c = (int)(i - slot * q) * 4;
+    const int32_t row = row_ids[slot];
+    float4 a = *reinterpret_cast<const float4*>(seg_row(ep.prev0, row) + c);
+    for (int k = 0; k + 1 < ep.n_prev; ++k) {
+        const float4 t =
+            *reinterpret_cast<const float4*>(ep.prev_dense[k] + (int64_t)row * ep.ld_prev + c);
+        a.x = a.x + t.x;
+        a.y = a.y + t.y;
+        a.z = a.z + t.z;
+        a.w = a.w + t.w;
+    }
+    *reinterpret_cast<float4*>(S + (int64_t)row * lds + c) = a;
+}
+
+int presum_rows(const int32_t* row_ids, int32_t n_slots, const lgcn_epilogue_t& ep, int32_t d,
+                float* S, hipStream_t s) {
+    if (n_slots <= 0) return 0;
+    const int64_t n = (int64_t)n_slots * (d / 4);
+    hipLaunchKernelGGL(k_presum, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, row_ids,
+                       n_slots, ep, d, S, (int64_t)d);
+    return herr(hipGetLastError());
+}
+
 lgcn_rows_t dense_rows(const float* p, int32_t n, int64_t ld) {
     lgcn_rows_t r;
     r.p0 = r.p1 = r.p2 = p;
@@ -823,6 +856,10 @@ struct lgcn_sched {
     hipEvent_t piece_ev[2][LGCN_SCHED_MAX_PIECES];
     int chains_first;  // LGCN_SCHED_CHAINS_FIRST
     int lane_flip;     // LGCN_SCHED_LANE_FLIP: forward half-layer (k, side) on lane (k+side+K+1)%2
+    // LGCN_SCHED_PRESUM / _BUF: sides (bit s) whose mean half-layer reads one pre-summed row
+    // (written into presum_buf [n x d] right after the side's layer K-1)
+    int presum;
+    float* presum_buf;
 };
 
 namespace {
@@ -1284,6 +1321,13 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
         case LGCN_SCHED_MEAN_EARLY:
             sc->mean_early = value != 0;
             return 0;
+        case LGCN_SCHED_PRESUM:
+            if (value < 0 || value > 3) return LGCN_EINVAL;
+            sc->presum = (int)value;
+            return 0;
+        case LGCN_SCHED_PRESUM_BUF:
+            sc->presum_buf = reinterpret_cast<float*>(value);
+            return 0;
         case LGCN_SCHED_LANE_FLIP:
             sc->lane_flip = value != 0;
             return 0;
@@ -1395,6 +1439,16 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
         // only; the two sides of one layer are independent)
         for (int side = 1; side >= 0; --side) {
             const Lane& L = lanes[(k + side + K + (sched && sched->lane_flip ? 1 : 0)) & 1];
+            // PRESUM: the side's mean reads S = ((E0 + E1) + ...) + E_{K-1}, summed right after
+            // its layer K-1 (below) on that lane — one row read instead of K, same rounding
+            bool presum = two && K >= 2 && sched->presum_buf && ((sched->presum >> side) & 1) &&
+                          d % 4 == 0 && rows_aligned(emb) && al16(sched->presum_buf);
+            for (int i = 0; presum && i + 1 < K; ++i) presum = al16(layer_bufs_host[i]);
+            lgcn_epilogue_t eps = ep;
+            if (presum && k == K) {
+                eps.prev0 = dense_rows(sched->presum_buf, n, d);
+                eps.n_prev = 1;
+            }
             // the mean of a side reads its layer K-1, computed on the other lane: the half-layer
             // waits for it — or, with MEAN_EARLY, only its kernels that write Y do
             hipEvent_t late = nullptr;
@@ -1405,8 +1459,19 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
                     return e;
             }
             if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, x, 1.f,
-                                   nullptr, y, d, ep, sched, L, late))
+                                   nullptr, y, d, presum && k == K ? eps : ep, sched, L, late))
                 return e;
+            if (presum && k == K - 1) {
+                lgcn_epilogue_t pe;
+                memset(&pe, 0, sizeof(pe));
+                pe.prev0 = emb;
+                pe.n_prev = K;
+                for (int i = 0; i + 1 < K; ++i) pe.prev_dense[i] = layer_bufs_host[i];
+                pe.ld_prev = d;
+                const int32_t s0 = side ? split : 0, s1 = side ? n : split;
+                if (int e = presum_rows(row_ids + s0, s1 - s0, pe, d, sched->presum_buf, L.main))
+                    return e;
+            }
             if (two && k == K - 1)
                 if (int e = herr(hipEventRecord(sched->cross[side], L.main))) return e;
         }

@@ -29,6 +29,7 @@ SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, S
     1, 2, 3, 4, 5, 6
 SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST, SCHED_MEAN_EARLY = 7, 8, 9, 10
 SCHED_PIECES, SCHED_CHAINS_FIRST, SCHED_LANE_FLIP = 11, 12, 13
+SCHED_PRESUM, SCHED_PRESUM_BUF = 14, 15
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
@@ -986,6 +987,14 @@ def sched_for(device, n_aux=None):
     return _scheds[key]
 
 
+def presum_sides():
+    """Sides whose final mean reads a pre-summed row (LGCN_PRESUM, bit s = side s; default 0 =
+    off: at C3 the users' presum (10.5 GB right after their layer 2) slows the items' layer 2,
+    the critical path, more than it saves in layer 3: forward 12.78 -> 13.3 ms with bit 0)."""
+    v = os.environ.get("LGCN_PRESUM", "0")
+    return max(0, min(3, int(v))) if v.strip() else 0
+
+
 def sched_pieces():
     """Chunk windows of the pipelined block pass + walk of parts 0 and 1 (LGCN_PIECES, 0..4;
     0/1 = each part's block pass, then its walk)."""
@@ -1195,6 +1204,15 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
             _note_schedule(sc, True)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
+            presum = None
+            if sc is not None:
+                # the users' mean reads one pre-summed row (LGCN_SCHED_PRESUM); the buffer lives
+                # until the lanes are joined back into `stream` (lgcn_propagate_forward_sides)
+                mask = presum_sides() if K >= 2 else 0
+                if mask:
+                    presum = torch.empty((n, d), dtype=torch.float32, device=dev)
+                sc.set(SCHED_PRESUM, mask)
+                sc.set(SCHED_PRESUM_BUF, presum.data_ptr() if presum is not None else 0)
             try:
                 _check(lib.lgcn_propagate_forward_sides(
                     _ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), n, graph.split,

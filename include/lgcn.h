@@ -489,6 +489,14 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        streams) then carries the chain ending in layer K's side 0
                                        (users: the mean over the most rows, after the items' layer
                                        K-1); 0 (the C default): (k + side + K) % 2 */
+#define LGCN_SCHED_PRESUM       14  /* bit s: lgcn_propagate_forward_sides writes side s's rows of
+                                       S = ((E0 + E1) + ...) + E_{K-1} into the PRESUM_BUF buffer
+                                       right after its layer K-1 (on that lane, before the other
+                                       lane's mean half-layer is released), and side s's mean
+                                       then reads S (one row instead of K; same rounding). Needs
+                                       the two lanes, K >= 2, d % 4 == 0, 16-B aligned E0 segments
+                                       and buffers; 0 (the C default): off */
+#define LGCN_SCHED_PRESUM_BUF   15  /* float* [n x d] (row ids, ld = d) for LGCN_SCHED_PRESUM */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +
