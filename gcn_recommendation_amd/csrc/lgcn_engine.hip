@@ -30,6 +30,7 @@ int g_unroll = 0;
 int g_mean_prefetch = 0;
 int g_min_groups = 0;
 int g_emu_resolve = 0;  // LGCN_TUNE_EMU_RESOLVE (read by lgcn_exact.hip's walk launch)
+int g_emu_margin = (128 << 4) | 4;  // LGCN_TUNE_EMU_MARGIN (the walk's prediction margin)
 }  // namespace lgcn_detail
 
 namespace {
@@ -441,6 +442,11 @@ int lgcn_tune(int knob, int value) {
         case LGCN_TUNE_EMU_RESOLVE: {
             const int old = lgcn_detail::g_emu_resolve;
             if (value >= 0) lgcn_detail::g_emu_resolve = value;
+            return old;
+        }
+        case LGCN_TUNE_EMU_MARGIN: {
+            const int old = lgcn_detail::g_emu_margin;
+            if (value >= 0) lgcn_detail::g_emu_margin = value;
             return old;
         }
         default:
@@ -855,7 +861,8 @@ struct lgcn_sched {
     int pieces;
     hipEvent_t piece_ev[2][LGCN_SCHED_MAX_PIECES];
     int chains_first;  // LGCN_SCHED_CHAINS_FIRST
-    int lane_flip;     // LGCN_SCHED_LANE_FLIP: forward half-layer (k, side) on lane (k+side+K+1)%2
+    int lane_flip;     // LGCN_SCHED_LANE_FLIP bits 1 / 2: forward / backward half-layer (k, side)
+                       // on lane (k + side + K + 1) % 2
     // LGCN_SCHED_PRESUM / _BUF: sides (bit s) whose mean half-layer reads one pre-summed row
     // (written into presum_buf [n x d] right after the side's layer K-1)
     int presum;
@@ -1329,7 +1336,8 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
             sc->presum_buf = reinterpret_cast<float*>(value);
             return 0;
         case LGCN_SCHED_LANE_FLIP:
-            sc->lane_flip = value != 0;
+            if (value < 0 || value > 3) return LGCN_EINVAL;
+            sc->lane_flip = (int)value;
             return 0;
         case LGCN_SCHED_CHAINS_FIRST:
             sc->chains_first = value != 0;
@@ -1438,7 +1446,7 @@ int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges
         // the item side first: its half-layer holds the longest walks (host submission order
         // only; the two sides of one layer are independent)
         for (int side = 1; side >= 0; --side) {
-            const Lane& L = lanes[(k + side + K + (sched && sched->lane_flip ? 1 : 0)) & 1];
+            const Lane& L = lanes[(k + side + K + (sched && (sched->lane_flip & 1) ? 1 : 0)) & 1];
             // PRESUM: the side's mean reads S = ((E0 + E1) + ...) + E_{K-1}, summed right after
             // its layer K-1 (below) on that lane — one row read instead of K, same rounding
             bool presum = two && K >= 2 && sched->presum_buf && ((sched->presum >> side) & 1) &&
@@ -1511,7 +1519,8 @@ int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edge
         float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
         for (int side = 1; side >= 0; --side)
             if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, h, xdiv, x_nz,
-                                   y, d, ep, sched, lanes[(k + side + K) & 1]))
+                                   y, d, ep, sched,
+                                   lanes[(k + side + K + (sched && (sched->lane_flip & 2) ? 1 : 0)) & 1]))
                 return e;
         h = dense_rows(y, n, d);
         xdiv = 1.f;

@@ -46,6 +46,7 @@
 
 namespace lgcn_detail {
 extern int g_emu_resolve;  // LGCN_TUNE_EMU_RESOLVE (lgcn_engine.hip)
+extern int g_emu_margin;   // LGCN_TUNE_EMU_MARGIN (lgcn_engine.hip)
 }
 
 namespace {
@@ -606,6 +607,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
                                                  lgcn_epilogue_t ep, int NS, int max_it,
+                                                 int pmargin,
                                                  const lgcn_emu_row_t* __restrict__ live,
                                                  int32_t ch_lo, int32_t ch_hi) {
     constexpr int CH = LGCN_EMU_CH;
@@ -731,7 +733,8 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
         const int wc = inw ? w : 0;
         const int lo = m.x >> wc, hi = -((-m.y) >> wc);
         const int alo = neg ? -hi : lo, ahi = neg ? -lo : hi;
-        const int mg = ((hi - lo) >> 3) + 256;
+        // widened bounds: (hi - lo) >> shift + base (pmargin = base << 4 | shift; default 4, 128)
+        const int mg = ((hi - lo) >> (pmargin & 15)) + (pmargin >> 4);
         bool ok = ident || (inw && M + alo >= kLB + mg && M + ahi <= kHB - mg);
         LGCN_EMU_FORCE(ok);
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
@@ -1032,11 +1035,13 @@ int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     if (slots >= LGCN_WALK_ISO_SLOTS)
         hipLaunchKernelGGL((k_emu_walk<MODE, XD, true>), grid, dim3(64), lds, s, edges, blocks,
                            rows, ktab, meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
-                           lgcn_detail::g_emu_resolve, live, ch_lo, ch_hi);
+                           lgcn_detail::g_emu_resolve,
+                           lgcn_detail::g_emu_margin, live, ch_lo, ch_hi);
     else
         hipLaunchKernelGGL((k_emu_walk<MODE, XD, false>), grid, dim3(64), lds, s, edges, blocks,
                            rows, ktab, meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
-                           lgcn_detail::g_emu_resolve, live, ch_lo, ch_hi);
+                           lgcn_detail::g_emu_resolve,
+                           lgcn_detail::g_emu_margin, live, ch_lo, ch_hi);
     return herr_x(hipGetLastError());
 }
 

@@ -25,6 +25,7 @@ COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
 TUNE_EMU_RESOLVE = 5
+TUNE_EMU_MARGIN = 6
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
 SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST, SCHED_MEAN_EARLY = 7, 8, 9, 10
@@ -231,6 +232,10 @@ def load_library(path=None):
         # LGCN_EMU_RESOLVE=k: A/B switch of the walk's parallel runs per resolved block (same bits)
         if os.environ.get("LGCN_EMU_RESOLVE", ""):
             lib.lgcn_tune(TUNE_EMU_RESOLVE, int(os.environ["LGCN_EMU_RESOLVE"]))
+        # LGCN_EMU_MARGIN=shift:base: A/B of the walk's prediction margin (same bits)
+        if os.environ.get("LGCN_EMU_MARGIN", ""):
+            sh, base = (int(t) for t in os.environ["LGCN_EMU_MARGIN"].split(":"))
+            lib.lgcn_tune(TUNE_EMU_MARGIN, (base << 4) | sh)
         _lib = lib
         return lib
 
@@ -946,7 +951,7 @@ class Sched:
         # LGCN_CHAINS_FIRST=1: a half-layer without walks (C3's users) runs its chain rows before
         # its layer kernel (A/B: 13.7 ms best case at C3 but bimodal under the lane priorities)
         self.set(SCHED_CHAINS_FIRST, 1 if os.environ.get("LGCN_CHAINS_FIRST", "0") == "1" else 0)
-        self.set(SCHED_LANE_FLIP, 1 if os.environ.get("LGCN_LANE_FLIP", "0") == "1" else 0)
+        self.set(SCHED_LANE_FLIP, int(os.environ.get("LGCN_LANE_FLIP", "0") or 0))
 
     def set(self, knob, value):
         _check(self.lib.lgcn_sched_set(self.handle, knob, int(value)), "lgcn_sched_set")

@@ -226,6 +226,10 @@ const char* lgcn_error_string(int code);
 #define LGCN_TUNE_EMU_RESOLVE    5  /* emulation walk: parallel exact-step runs per block it must
                                        resolve before the rest runs as the sequential chain
                                        (default 0: always the sequential chain) */
+#define LGCN_TUNE_EMU_MARGIN     6  /* emulation walk: the prediction's widened bounds, base << 4 |
+                                       shift: (hi - lo) >> shift + base (default 128 << 4 | 4;
+                                       A/B at C3: 3,256 / 2,256 / 3,1024 / 2,2048 within noise);
+                                       results identical for every value (prediction only) */
 int lgcn_tune(int knob, int value);
 
 /* device properties the host side needs (CU count); returns 0/hipError */
@@ -484,11 +488,11 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        chain rows on the caller's stream before the layer kernel
                                        (beside it on an aux stream they are dispatched only once
                                        the layer kernel's grid is); 0 (the C default): beside */
-#define LGCN_SCHED_LANE_FLIP    13  /* 1: lgcn_propagate_forward_sides runs half-layer (k, side) on
-                                       lane (k + side + K + 1) % 2 — lane 1 (the high-priority
-                                       streams) then carries the chain ending in layer K's side 0
-                                       (users: the mean over the most rows, after the items' layer
-                                       K-1); 0 (the C default): (k + side + K) % 2 */
+#define LGCN_SCHED_LANE_FLIP    13  /* bit 1 (forward) / bit 2 (backward): lgcn_propagate_*_sides
+                                       runs half-layer (k, side) on lane (k + side + K + 1) % 2 —
+                                       lane 1 (the high-priority streams) then carries the chain
+                                       ending in layer K's side 0; 0 (the C default):
+                                       (k + side + K) % 2 */
 #define LGCN_SCHED_PRESUM       14  /* bit s: lgcn_propagate_forward_sides writes side s's rows of
                                        S = ((E0 + E1) + ...) + E_{K-1} into the PRESUM_BUF buffer
                                        right after its layer K-1 (on that lane, before the other
