@@ -22,14 +22,15 @@ import time
 # streams are high priority: every stream gets a queue under the default, which is what
 # main.py runs with (round 4: 17.08 ms at 4 queues vs 17.17 ms at 8). The environment is left
 # alone; LGCN_HW_QUEUES=N sets GPU_MAX_HW_QUEUES for an A/B.
-# Under torch.distributed (N > 1, or --force-dist) RCCL's own stream takes one of the
-# normal-priority queues, and the caller's + aux 0..2 would share the other three (world-1
-# featsplit 16.0 ms vs 13.4 ms for the same shard forward without RCCL): there the process asks
-# for 8 per priority before the GPU is touched, unless the environment already sets it.
+# Under torch.distributed (N > 1, or --force-dist) RCCL's communicator holds streams of its own,
+# which then share HIP's hardware queues with the two lanes' streams: world-1 featsplit over
+# RCCL 15.8 / 16.3 ms at GPU_MAX_HW_QUEUES = 4 / 8 vs 13.2 ms over gloo, 13.1 ms over RCCL at
+# 16. There the process asks for 16 per priority before the GPU is touched, unless the
+# environment already sets it.
 if os.environ.get("LGCN_HW_QUEUES", ""):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LGCN_HW_QUEUES"]
 elif int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--force-dist" in sys.argv:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 import numpy as np
 import torch
