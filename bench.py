@@ -25,12 +25,16 @@ import time
 # Under torch.distributed (N > 1, or --force-dist) RCCL's communicator holds streams of its own,
 # which then share HIP's hardware queues with the two lanes' streams: world-1 featsplit over
 # RCCL 15.8 / 16.3 ms at GPU_MAX_HW_QUEUES = 4 / 8 vs 13.2 ms over gloo, 13.1 ms over RCCL at
-# 16. There the process asks for 16 per priority before the GPU is touched, unless the
-# environment already sets it.
+# 16. There the process raises it to 16 per priority before the GPU is touched (an environment
+# that already asks for more keeps its value).
 if os.environ.get("LGCN_HW_QUEUES", ""):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["LGCN_HW_QUEUES"]
 elif int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--force-dist" in sys.argv:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    try:
+        _q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        _q = 4
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(_q, 16))
 
 import numpy as np
 import torch
