@@ -47,7 +47,9 @@ def main():
     gen = torch.Generator().manual_seed(42)
     segs = [bench.xavier(U, d, gen).to(dev), bench.xavier(I, d, gen).to(dev)]
     # the C host's objects: 4 plans (2 sides x 2 scratch sets), the schedule, the buffers
-    plans, _ = engine._side_plans(g, d, 128, "exact", 0, True)
+    # (the plans the engine builds: at C3 scale rows of 129..1024 edges are whole-row items of
+    # the layer kernel, emu_min = engine.emu_min_degree_from_env(nnz))
+    plans, _ = engine._side_plans(g, d, 128, "exact", engine.emu_min_degree_from_env(g.nnz), True)
     sc = engine.sched_for(dev)
     layers = [torch.empty((n, d), device=dev) for _ in range(K - 1)]
     out_c = torch.empty((n, d), device=dev)
