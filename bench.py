@@ -562,7 +562,8 @@ def main():
     def timed(mode, steps, warmup):
         """(ms per step, [steps x K] layer ms, [steps x K] layer-kernel ms, output). Sided: no
         layer boundary exists (the two lanes overlap layers), layer ms is None and the kernel ms
-        are [steps x K x 2] — each half-layer's layer kernel, timed on its lane's stream."""
+        are [steps x K x 4] — each segment's layer kernel (the side-0 classes, side 1), timed on
+        its lane's stream (0 for an empty segment)."""
         for _ in range(warmup):
             step(mode=mode)
         torch.cuda.synchronize()
@@ -585,7 +586,8 @@ def main():
                 step(None, None, mode)
             torch.cuda.synchronize()
             tm, engine.side_timing = engine.side_timing, None
-            ker = np.array([[[t[(k, s)][0].elapsed_time(t[(k, s)][1]) for s in (0, 1)]
+            ker = np.array([[[t[(k, s)][0].elapsed_time(t[(k, s)][1]) if (k, s) in t else 0.0
+                              for s in range(engine.N_SEGS)]
                              for k in range(1, K + 1)] for t in tm])
             return a_.elapsed_time(b_) / steps, None, ker, o
         lay = np.array([[x.elapsed_time(y) for x, y in st] for st in evs])
@@ -599,9 +601,9 @@ def main():
         fn()
         torch.cuda.synchronize()
         tr, engine.side_trace = engine.side_trace[0], None
-        t0_ = tr[(1, 0)][0][1]
-        return {f"layer{k}_side{s}_lane{(k + s + K) % 2}":
-                {nm: round(t0_.elapsed_time(ev), 3) for nm, ev in tr[(k, s)][1:]}
+        t0_ = tr[min(tr)][0][1]
+        return {f"layer{k}_seg{s}_lane{(k + (s == 3) + K) % 2}":
+                {nm: round(t0_.elapsed_time(ev), 3) for nm, ev in tr[(k, s)]}
                 for (k, s) in sorted(tr)}
 
     # the headline: the engine's default (exact) hub mode — every row bitwise the reference's
@@ -620,21 +622,29 @@ def main():
     # FETCH_SIZE + WRITE_SIZE, stamped with the hash of the kernel sources; a stale file is
     # refused) / launch time / peak. Algorithmic bytes are reported beside it.
     # algorithmic bytes of one layer-kernel launch (SURVEY §8d per-edge model over the rows the
-    # kernel itself runs — bundle rows, degree <= threshold; hub rows run beside it): gathered
-    # X rows (4d) + edge records (8) per edge, row pointers, one written row per bundle row
+    # kernel itself runs — bundle rows (degree <= threshold) and, in the exact plan, the
+    # whole-row items up to emu_min_degree; longer rows run beside it): gathered X rows (4d) +
+    # edge records (8) per edge, row pointers, one written row per row it runs
     rp_h = g.rowptr_host().astype(np.int64)
+    emu_min = engine.emu_min_degree_from_env(nnz)
 
     def kernel_bytes(s0, s1):
         deg_ = np.diff(rp_h[s0:s1 + 1])
-        bun = deg_ <= min(hub_thr, engine.INT32_MAX)
-        return int(deg_[bun].sum()) * (4 * d + 8) + 4 * (s1 - s0 + 1) + 4 * int(bun.sum()) * d
+        run = deg_ <= max(min(hub_thr, engine.INT32_MAX), emu_min if hub_mode == "exact" else 0)
+        return int(deg_[run].sum()) * (4 * d + 8) + 4 * (s1 - s0 + 1) + 4 * int(run.sum()) * d
     if sided:
-        b_side = [kernel_bytes(0, g.split), kernel_bytes(g.split, n)]
-        b_layer = sum(b_side) / 2          # per launch, averaged over the two sides' launches
-        store_ms = float(kern_ms[:, :-1, :].mean()) if K > 1 else float(kern_ms.mean())
-        mean_ms = float(kern_ms[:, -1, :].mean())
-        kname = (f"k_layer<float4,{min(64, d // 4)},{max(1, d // 256)},STORE> half-layer launches "
-                 f"(layers 1..K-1, both sides: bundle rows of the users / items)")
+        segs_ = g.segments()
+        b_seg = [kernel_bytes(a, b) if b > a else 0 for a, b in segs_]
+        live_ = [gi for gi, (a, b) in enumerate(segs_) if b > a]
+        # STORE launches: layers 1..K-1, every non-empty segment; bytes and time summed over them
+        st_k = kern_ms[:, :-1, :] if K > 1 else kern_ms
+        n_launch = len(live_) * st_k.shape[1]
+        store_ms = float(st_k.sum(axis=(1, 2)).mean()) / max(n_launch, 1)
+        b_layer = sum(b_seg[gi] for gi in live_) * st_k.shape[1] / max(n_launch, 1)
+        mean_ms = float(kern_ms[:, -1, :].sum(axis=1).mean()) / max(len(live_), 1)
+        kname = (f"k_layer<float4,{min(64, d // 4)},{max(1, d // 256)},STORE> segment launches "
+                 f"(layers 1..K-1: the users' classes and the items; bundle rows and whole-row "
+                 f"items up to {emu_min} edges)")
     else:
         b_layer = kernel_bytes(0, n)
         store_ms = float(kern_ms[:, :-1].mean()) if K > 1 else float(kern_ms.mean())
@@ -651,9 +661,10 @@ def main():
                                     "measured rate when hot gathered rows hit L2/MALL"},
             "mean_layer": {"avg_launch_ms": round(mean_ms, 4)}}
     if sided:
-        roof["half_layer_kernel_ms"] = {f"layer{k + 1}": [round(float(x), 4) for x in row]
-                                        for k, row in enumerate(kern_ms.mean(0))}
-        roof["algorithmic"]["bytes_per_side"] = b_side
+        roof["segment_kernel_ms"] = {f"layer{k + 1}": [round(float(x), 4) for x in row]
+                                     for k, row in enumerate(kern_ms.mean(0))}
+        roof["algorithmic"]["bytes_per_segment"] = b_seg
+        roof["algorithmic"]["launches_per_step"] = n_launch
         roof["note"] = ("the layer kernel's time (and so frac) is measured as it runs, sharing "
                         "the GPU with the emulation kernels and the other lane")
     else:
@@ -696,6 +707,8 @@ def main():
                    "hub_threshold": hub_thr, "hub_mode": hub_mode,
                    "emu_min_degree": engine.emu_min_degree_from_env(nnz),
                    "schedule": ("bipartite two-lane (lgcn_propagate_forward_sides), "
+                                f"side-0 classes {list(g.class_end or ())} (parts "
+                                f"{list(g.class_parts)}), "
                                 f"{engine.n_aux_streams()} aux streams, GPU_MAX_HW_QUEUES="
                                 f"{os.environ.get('GPU_MAX_HW_QUEUES', 'unset (HIP default 4)')}") if sided else "one operator",
                    "parallelism": "single"},

@@ -21,6 +21,7 @@
 
 #include <string.h>
 #include <algorithm>
+#include <functional>
 #include <new>
 #include <vector>
 
@@ -29,7 +30,6 @@ int g_rows_per_group = 0;
 int g_unroll = 0;
 int g_mean_prefetch = 0;
 int g_min_groups = 0;
-int g_emu_resolve = 0;  // LGCN_TUNE_EMU_RESOLVE (read by lgcn_exact.hip's walk launch)
 int g_emu_margin = (128 << 4) | 4;  // LGCN_TUNE_EMU_MARGIN (the walk's prediction margin)
 }  // namespace lgcn_detail
 
@@ -214,6 +214,66 @@ __global__ void k_csr_relabel_cols(const lgcn_edge_t* __restrict__ edges, int64_
 }
 
 // ---------------------------------------------------------------------------------------------
+// side-0 classes of a bipartite slot order (lgcn_csr_side_classes): a side-0 row (user / brand)
+// is class 0 when it is linked to a side-1 row of part 0 (the longest, walked item rows), class 1
+// when linked to a part-1 row only, class 2 otherwise. Stored class-major (each class keeps its
+// degree order), the half-layers of side 0 run one class at a time, and a walked part of the
+// next side-1 half-layer waits only for the classes it reads (lgcn_propagate_*_sides).
+// ---------------------------------------------------------------------------------------------
+__global__ void k_fill_i32(int32_t* __restrict__ p, int64_t n, int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// mark[col] = min(mark[col], part) for every edge of side-1 slot s_lo + blockIdx.x (part 0 below
+// s_mid, 1 above); gridDim.y blocks stride over the slot's edges
+__global__ void k_class_mark(const int32_t* __restrict__ rowptr,
+                             const lgcn_edge_t* __restrict__ edges, int32_t s_lo, int32_t s_mid,
+                             int32_t* __restrict__ mark) {
+    const int32_t slot = s_lo + (int32_t)blockIdx.x;
+    const int32_t part = slot < s_mid ? 0 : 1;
+    const int64_t end = rowptr[slot + 1];
+    for (int64_t j = rowptr[slot] + (int64_t)blockIdx.y * blockDim.x + threadIdx.x; j < end;
+         j += (int64_t)gridDim.y * blockDim.x)
+        atomicMin(mark + load_edge(edges + j).x, part);
+}
+
+__global__ void k_class_keys(const int32_t* __restrict__ row_ids, const int32_t* __restrict__ mark,
+                             int32_t n0, int32_t* __restrict__ key, int32_t* __restrict__ iota) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n0) return;
+    key[s] = mark[row_ids[s]];
+    iota[s] = (int32_t)s;
+}
+
+// the new slot s takes old slot src = perm0[s] (side 0, class-sorted) or s (side 1)
+__global__ void k_class_apply(const int32_t* __restrict__ perm0, const int32_t* __restrict__ rowptr,
+                              const int32_t* __restrict__ row_ids, int32_t split, int32_t n,
+                              int32_t* __restrict__ perm, int32_t* __restrict__ deg,
+                              int32_t* __restrict__ row_ids_out) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int32_t src = s < split ? perm0[s] : (int32_t)s;
+    perm[s] = src;
+    deg[s] = rowptr[src + 1] - rowptr[src];
+    row_ids_out[s] = row_ids[src];
+}
+
+// class_end[c] = first side-0 slot of a class above c (keys sorted ascending); one thread
+__global__ void k_class_bounds(const int32_t* __restrict__ key_sorted, int32_t n0,
+                               int32_t* __restrict__ class_end) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int c = 0; c < 2; ++c) {
+        int32_t a = 0, b = n0;
+        while (a < b) {
+            const int32_t mid = (a + b) >> 1;
+            if (key_sorted[mid] <= c) a = mid + 1; else b = mid;
+        }
+        class_end[c] = a;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // adjacency builder (main.py:313-336 on the device): degree histogram, duplicate merge by a
 // 64-bit radix sort of row*n+col keys + run-length encode, values fp32((d_r * m) * d_c)
 // ---------------------------------------------------------------------------------------------
@@ -362,39 +422,6 @@ int scale_rows(const lgcn_rows_t& x, int32_t n_rows, int32_t d, float div, float
     return dispatch_geo(g, f);
 }
 
-// S[row] = ((P0[row] + P1[row]) + ...) + P_{n-1}[row] (ep.prev0, ep.prev_dense: the first n_prev
-// terms of a MEAN epilogue, in its order) for the rows of slots [0, n_slots): a side's layer-K
-// mean then reads one row instead of n_prev (LGCN_SCHED_PRESUM). One float4 per thread.
-__global__ __launch_bounds__(256) void k_presum(const int32_t* __restrict__ row_ids,
-                                                int32_t n_slots, lgcn_epilogue_t ep, int32_t d,
-                                                float* __restrict__ S, int64_t lds) {
-    const int q = d >> 2;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t slot = i / q;
-    if (slot >= n_slots) return;
-    const int c = (int)(i - slot * q) * 4;
-    const int32_t row = row_ids[slot];
-    float4 a = *reinterpret_cast<const float4*>(seg_row(ep.prev0, row) + c);
-    for (int k = 0; k + 1 < ep.n_prev; ++k) {
-        const float4 t =
-            *reinterpret_cast<const float4*>(ep.prev_dense[k] + (int64_t)row * ep.ld_prev + c);
-        a.x = a.x + t.x;
-        a.y = a.y + t.y;
-        a.z = a.z + t.z;
-        a.w = a.w + t.w;
-    }
-    *reinterpret_cast<float4*>(S + (int64_t)row * lds + c) = a;
-}
-
-int presum_rows(const int32_t* row_ids, int32_t n_slots, const lgcn_epilogue_t& ep, int32_t d,
-                float* S, hipStream_t s) {
-    if (n_slots <= 0) return 0;
-    const int64_t n = (int64_t)n_slots * (d / 4);
-    hipLaunchKernelGGL(k_presum, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, row_ids,
-                       n_slots, ep, d, S, (int64_t)d);
-    return herr(hipGetLastError());
-}
-
 lgcn_rows_t dense_rows(const float* p, int32_t n, int64_t ld) {
     lgcn_rows_t r;
     r.p0 = r.p1 = r.p2 = p;
@@ -437,11 +464,6 @@ int lgcn_tune(int knob, int value) {
         case LGCN_TUNE_MIN_GROUPS: {
             const int old = lgcn_detail::g_min_groups;
             if (value >= 0) lgcn_detail::g_min_groups = value;
-            return old;
-        }
-        case LGCN_TUNE_EMU_RESOLVE: {
-            const int old = lgcn_detail::g_emu_resolve;
-            if (value >= 0) lgcn_detail::g_emu_resolve = value;
             return old;
         }
         case LGCN_TUNE_EMU_MARGIN: {
@@ -711,6 +733,72 @@ int lgcn_csr_check_bipartite(const int32_t* rowptr, const lgcn_edge_t* edges,
     return last_err();
 }
 
+int lgcn_csr_side_classes(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                          int32_t n_rows, int64_t nnz, int32_t split, int32_t part_rows0,
+                          int32_t part_rows1, int32_t* work, int32_t* row_ids_out,
+                          int32_t* rowptr_out, lgcn_edge_t* edges_out, int32_t* class_end,
+                          void* temp, size_t* temp_bytes_host, void* stream) {
+    if (n_rows < 0 || nnz < 0 || nnz > 0x7fffffffLL || !temp_bytes_host) return LGCN_EINVAL;
+    if (split < 0 || split > n_rows || part_rows0 < 0 || part_rows0 > part_rows1 ||
+        part_rows1 > n_rows - split)
+        return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    const int32_t n = n_rows, n0 = split;
+    int32_t* mark = work;
+    int32_t* key = work + n;
+    int32_t* key_sorted = work + 2 * (int64_t)n;
+    int32_t* iota = work + 3 * (int64_t)n;
+    int32_t* perm0 = work + 4 * (int64_t)n;
+    if (temp == nullptr) {
+        size_t b1 = 0, b2 = 0;
+        hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b1, key, key_sorted, iota,
+                                                          perm0, n0, 0, 2, s);
+        if (e != hipSuccess) return (int)e;
+        e = hipcub::DeviceScan::InclusiveSum(nullptr, b2, key, rowptr_out, n, s);
+        if (e != hipSuccess) return (int)e;
+        *temp_bytes_host = std::max(b1, b2);
+        return 0;
+    }
+    if (!rowptr || !rowptr_out || !row_ids_out || !class_end || !work ||
+        (n > 0 && !row_ids) || (nnz > 0 && (!edges || !edges_out)))
+        return LGCN_EINVAL;
+    if (int e = herr(hipMemsetAsync(rowptr_out, 0, sizeof(int32_t), s))) return e;
+    if (int e = herr(hipMemsetAsync(class_end, 0, 2 * sizeof(int32_t), s))) return e;
+    if (n == 0) return 0;
+    auto grid = [](int64_t m) { return dim3((uint32_t)((m + kBlock - 1) / kBlock)); };
+    hipLaunchKernelGGL(k_fill_i32, grid(n), dim3(kBlock), 0, s, mark, (int64_t)n, 2);
+    if (int e = last_err()) return e;
+    if (part_rows1 > 0) {
+        hipLaunchKernelGGL(k_class_mark, dim3((uint32_t)part_rows1, 256), dim3(kBlock), 0, s, rowptr,
+                           edges, split, split + part_rows0, mark);
+        if (int e = last_err()) return e;
+    }
+    if (n0 > 0) {
+        hipLaunchKernelGGL(k_class_keys, grid(n0), dim3(kBlock), 0, s, row_ids, mark, n0, key, iota);
+        if (int e = last_err()) return e;
+        size_t bytes = *temp_bytes_host;
+        // LSD radix sort: stable, so every class keeps the degree order of its rows
+        if (int e = herr(hipcub::DeviceRadixSort::SortPairs(temp, bytes, key, key_sorted, iota,
+                                                            perm0, n0, 0, 2, s)))
+            return e;
+        hipLaunchKernelGGL(k_class_bounds, dim3(1), dim3(64), 0, s, key_sorted, n0, class_end);
+        if (int e = last_err()) return e;
+    }
+    // full permutation (key: new slot -> old slot) and the degrees in the new order
+    int32_t* perm = key;
+    int32_t* deg = iota;
+    hipLaunchKernelGGL(k_class_apply, grid(n), dim3(kBlock), 0, s, perm0, rowptr, row_ids, n0, n,
+                       perm, deg, row_ids_out);
+    if (int e = last_err()) return e;
+    size_t bytes = *temp_bytes_host;
+    if (int e = herr(hipcub::DeviceScan::InclusiveSum(temp, bytes, deg, rowptr_out + 1, n, s)))
+        return e;
+    if (nnz == 0) return 0;
+    hipLaunchKernelGGL(k_csr_gather_rows, grid(nnz), dim3(kBlock), 0, s, rowptr_out, perm, rowptr,
+                       edges, n, nnz, edges_out);
+    return last_err();
+}
+
 int lgcn_csr_relabel_cols(const lgcn_edge_t* edges, int64_t nnz, const int32_t* new_id,
                           lgcn_edge_t* edges_out, void* stream) {
     if (nnz < 0 || (nnz > 0 && (!edges || !new_id || !edges_out))) return LGCN_EINVAL;
@@ -825,54 +913,94 @@ int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* 
 
 }  // extern "C"
 
-// The concurrent schedule of an exact layer (lgcn_sched_create): auxiliary streams the emulated
-// and chain rows run on beside the layer kernel, and the events that fork them from the caller's
-// stream and join them back (graph-capture safe: a captured fork/join is a graph dependency).
-#define LGCN_SCHED_MAX_PIECES 4
+// ---------------------------------------------------------------------------------------------
+// The concurrent schedule of the exact layers (lgcn_sched_create): auxiliary streams the
+// emulated and chain rows run on beside the layer kernel, the bipartite lanes, and the events
+// that fork and join them (graph-capture safe: a captured fork/join is a graph dependency).
+// ---------------------------------------------------------------------------------------------
+namespace {
+// Every event record of one call takes a fresh event from this pool, so no event is recorded
+// twice inside one call (a captured graph's edges follow the records one to one); the next call
+// starts over. Created by lgcn_sched_create — nothing is created while a stream is captured. A
+// call that needs more wraps around (eager runs stay ordered: a wait binds to the record before
+// it).
+constexpr int kPoolEvents = 1024;
+struct EventPool {
+    hipEvent_t ev[kPoolEvents];
+    int n = 0;
+    int next = 0;
+    int32_t state[4] = {0, 0, 0, 0};  // the latest call's schedule (lgcn_sched_state)
+};
+}  // namespace
+
 struct lgcn_sched {
     hipStream_t aux[3];
     int n_aux;
-    hipEvent_t fork;
-    hipEvent_t join[3];
+    EventPool* pool;        // owned by the root schedule; lane 1's view shares it
     int32_t slots[2];       // walk LDS slots of part 0 / part 1 (0 = default)
     int chain;              // 0: chain rows are walked too (tests / A-B)
     hipEvent_t t0, t1;      // optional: recorded on the caller's stream around the layer kernel
     hipEvent_t* trace;      // optional [8]: phase events (LGCN_SCHED_TRACE)
     // bipartite lanes (lgcn_propagate_*_sides; created with >= 4 aux streams): the second lane's
-    // main stream and its own view (aux streams + fork/join events), the events that fork it
-    // from / join it into the caller's stream, and cross[side]: a side's layer K-1 done (the
-    // final mean half-layer of that side, on the other lane, waits for it)
+    // main stream and its own view (aux streams)
     hipStream_t lane1_main;
     lgcn_sched* lane1;
-    hipEvent_t lane_fork, lane_join, cross[2];
-    hipEvent_t* trace_sides;  // optional [16 K] (LGCN_SCHED_TRACE_SIDES)
-    hipEvent_t* timing_sides; // optional [4 K] (LGCN_SCHED_TIMING_SIDES)
-    // LGCN_SCHED_BLOCKS_FIRST: the layer kernel waits for part 0's block pass (blocks_done), so
-    // the longest rows' walk starts before the layer kernel floods the chip
-    int blocks_first;
-    hipEvent_t blocks_done;
-    // LGCN_SCHED_MEAN_EARLY: a final (mean) half-layer forks its block passes before it waits for
-    // the other lane's layer K-1; only the kernels that write Y wait (`late`, set per half-layer)
-    int mean_early;
-    hipEvent_t late;
-    // LGCN_SCHED_PIECES: parts 0 and 1 run their block pass and walk in `pieces` chunk windows
-    // (block pass windows on the caller's stream, piece_ev[part][j] after window j; the walk of
-    // window j waits for it), so a walk starts after the block pass of its first chunks
-    int pieces;
-    hipEvent_t piece_ev[2][LGCN_SCHED_MAX_PIECES];
-    int chains_first;  // LGCN_SCHED_CHAINS_FIRST
-    int lane_flip;     // LGCN_SCHED_LANE_FLIP bits 1 / 2: forward / backward half-layer (k, side)
-                       // on lane (k + side + K + 1) % 2
-    // LGCN_SCHED_PRESUM / _BUF: sides (bit s) whose mean half-layer reads one pre-summed row
-    // (written into presum_buf [n x d] right after the side's layer K-1)
-    int presum;
-    float* presum_buf;
+    hipEvent_t* trace_sides;   // optional [32 K] (LGCN_SCHED_TRACE_SIDES)
+    hipEvent_t* timing_sides;  // optional [8 K] (LGCN_SCHED_TIMING_SIDES)
+    int classes;               // LGCN_SCHED_CLASSES (default 1)
+    int capture_aux;           // LGCN_SCHED_CAPTURE_AUX (default 0)
 };
 
 namespace {
 struct EmuPart {
     int32_t r0, r1, b0, b1;
 };
+
+int ev_next(const lgcn_sched* sc, hipEvent_t* e) {
+    EventPool* p = sc->pool;
+    if (p->n <= 0) return LGCN_EINVAL;
+    if (p->next >= p->n) p->next = 0;
+    *e = p->ev[p->next++];
+    return 0;
+}
+
+// an event recorded on `from` that `to` waits for
+int link(const lgcn_sched* sc, hipStream_t from, hipStream_t to) {
+    hipEvent_t e;
+    if (int r = ev_next(sc, &e)) return r;
+    if (int r = herr(hipEventRecord(e, from))) return r;
+    return herr(hipStreamWaitEvent(to, e, 0));
+}
+
+int record(const lgcn_sched* sc, hipStream_t st, hipEvent_t* out) {
+    if (int r = ev_next(sc, out)) return r;
+    return herr(hipEventRecord(*out, st));
+}
+
+int wait_ev(hipStream_t st, hipEvent_t e) { return e ? herr(hipStreamWaitEvent(st, e, 0)) : 0; }
+
+// Cross-stream dependencies of one layer under a schedule (all optional):
+//  - late: the epilogue's operands (a MEAN's earlier layers, made on the other lane) — every
+//    kernel that writes Y waits for them; the block passes (they read X only) do not;
+//  - part_wait[i]: walked part i (0, 1) reads only the X rows this event covers, so its block pass
+//    starts after it instead of after everything before the layer on `s`;
+//  - defer: parts 0 and 1 are not joined back into `s`; part_done[i] (written here) fires when
+//    part i's rows are written, and whoever reads them waits for it.
+// part_wait / defer take effect when parts 0, 1 and the chain rows have a stream each; otherwise
+// the parts fork and join with the rest and part_done fires with the joined layer.
+struct Deps {
+    hipEvent_t late[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t part_wait[2] = {nullptr, nullptr};
+    bool defer = false;
+    hipEvent_t part_done[2] = {nullptr, nullptr};
+};
+
+int wait_late(hipStream_t st, const Deps* dp) {
+    if (!dp) return 0;
+    for (hipEvent_t e : dp->late)
+        if (int r = wait_ev(st, e)) return r;
+    return 0;
+}
 
 // rows [r0, r1) of the emulated-row list: block pass (blocks [b0, b1)) into the scratch at the
 // part's block offset
@@ -911,12 +1039,14 @@ bool chain_ok(const lgcn_rows_t& x, int32_t d) {
 //    cannot take d / the alignment, or the schedule turns it off).
 // Without a schedule everything runs in that order on `s`. With one, the emulated parts run on
 // the auxiliary streams beside the layer kernel: part 0 (the longest rows, whose walk is the
-// layer's critical path) on aux[0], part 1 on aux[1], the chain rows on aux[2]; with fewer aux
-// streams the later parts share the last one.
+// layer's critical path) on aux[0], part 1 on aux[1], the chain rows on aux[2] (with fewer aux
+// streams the later parts share the last one); the block passes are enqueued first and the
+// layer kernel waits for part 0's, so the longest walk starts before the layer kernel fills the
+// chip (C3 forward 18.58 -> 18.06 ms, round 3).
 int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
                int32_t n, const lgcn_hub_plan_t& p, const lgcn_rows_t& x, float xdiv,
                const uint32_t* x_nz, float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t& ep,
-               const lgcn_sched* sc, hipStream_t s) {
+               const lgcn_sched* sc, hipStream_t s, Deps* dp = nullptr) {
     const int32_t ne = p.n_emu_rows;
     // row-sparse X (the backward's first layer on a BPR batch): every emulated row is a chain
     // over its live edges (lgcn_live_rows) — no block pass, no walk
@@ -925,10 +1055,6 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     // walked rows read the block-pass scratch, which must cover their blocks
     if ((chains || live ? p.emu_part_blocks[1] : p.n_emu_blocks) > p.emu_scratch_blocks)
         return LGCN_EINVAL;
-    // the operands of the epilogue are ready once `late` fires: without the concurrent block
-    // passes below, everything waits for it
-    if (sc && sc->late && (live || ne == 0))
-        if (int e = herr(hipStreamWaitEvent(s, sc->late, 0))) return e;
     hipEvent_t* tr = sc ? sc->trace : nullptr;
     auto mark = [&](int k, hipStream_t st) -> int {
         return tr && tr[k] ? herr(hipEventRecord(tr[k], st)) : 0;
@@ -939,15 +1065,13 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
                               {p.emu_part_rows[1], ne, p.emu_part_blocks[1], p.n_emu_blocks}};
     const int slots[3] = {sc ? sc->slots[0] : 0, sc ? sc->slots[1] : 0, sc ? sc->slots[1] : 0};
     auto layer_kernel = [&](hipStream_t st) -> int {
-        if (sc && sc->t0) {
+        if (sc && sc->t0)
             if (int e = herr(hipEventRecord(sc->t0, st))) return e;
-        }
         if (int e = spmm_layer(rowptr, edges, row_ids, n, p.threshold, p.items, p.n_items,
                                p.partials, x, y, ldy, d, ep, xdiv, x_nz, st))
             return e;
-        if (sc && sc->t1) {
+        if (sc && sc->t1)
             if (int e = herr(hipEventRecord(sc->t1, st))) return e;
-        }
         return hub_combine(p.rows, p.n_rows, p.n_pre, p.partials, y, ldy, d, ep, st);
     };
     auto chain_rows = [&](hipStream_t st) -> int {
@@ -969,37 +1093,45 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
         if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, lflags, st)) return e;
         return part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i], lflags, st);
     };
-    if (live) {
-        if (!sc) {
-            if (int e = live_rows(s)) return e;
+    // everything joined into `s`: the deferred parts are done with it
+    auto done_on_s = [&]() -> int {
+        if (dp && dp->defer && sc)
             for (int i = 0; i < 2; ++i)
-                if (int e = walked(i, s)) return e;
-            return layer_kernel(s);
-        }
+                if (int e = record(sc, s, &dp->part_done[i])) return e;
+        return 0;
+    };
+    if (!sc || ne == 0 || live) {
+        if (int e = wait_late(s, dp)) return e;
+    }
+    if (live && sc) {
         // aux[0]: the live-edge pass (its row flags gate the walks), then part 0's walk; aux[1]
         // (after the flags): part 1
         const int na = sc->n_aux;
         hipStream_t a0 = sc->aux[0], a1 = sc->aux[na > 1 ? 1 : 0];
         if (int e = mark(0, s)) return e;
-        if (int e = herr(hipEventRecord(sc->fork, s))) return e;
-        if (int e = herr(hipStreamWaitEvent(a0, sc->fork, 0))) return e;
+        if (int e = link(sc, s, a0)) return e;
         if (int e = live_rows(a0)) return e;
         if (int e = mark(4, a0)) return e;
-        if (a1 != a0) {
-            if (int e = herr(hipEventRecord(sc->join[0], a0))) return e;
-            if (int e = herr(hipStreamWaitEvent(a1, sc->join[0], 0))) return e;
-        }
+        if (a1 != a0)
+            if (int e = link(sc, a0, a1)) return e;
         if (int e = walked(0, a0)) return e;
         if (int e = mark(5, a0)) return e;
         if (int e = walked(1, a1)) return e;
         if (int e = mark(6, a1)) return e;
         if (int e = layer_kernel(s)) return e;
         if (int e = mark(3, s)) return e;
-        for (int i = 0; i < (a1 != a0 ? 2 : 1); ++i) {
-            if (int e = herr(hipEventRecord(sc->join[i], sc->aux[i]))) return e;
-            if (int e = herr(hipStreamWaitEvent(s, sc->join[i], 0))) return e;
-        }
-        return mark(7, s);
+        if (int e = link(sc, a0, s)) return e;
+        if (a1 != a0)
+            if (int e = link(sc, a1, s)) return e;
+        if (int e = mark(7, s)) return e;
+        return done_on_s();
+    }
+    if (live) {
+        if (int e = live_rows(s)) return e;
+        for (int i = 0; i < 2; ++i)
+            if (int e = walked(i, s)) return e;
+        if (int e = layer_kernel(s)) return e;
+        return done_on_s();
     }
     if (!sc || ne == 0) {
         for (int i = 0; i < 3; ++i)
@@ -1011,114 +1143,63 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
                 if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
                                       nullptr, s))
                     return e;
-        return chains ? chain_rows(s) : 0;
+        if (chains)
+            if (int e = chain_rows(s)) return e;
+        return done_on_s();
     }
-    // fork: X and the epilogue operands are ready on `s`
+    // fork: X is ready on `s` (parts 0 / 1 with a stream of their own: once their part_wait fires)
     const int na = sc->n_aux;
+    const bool own = dp && na >= 3;
     auto aux_of = [&](int part) { return sc->aux[part < na ? part : na - 1]; };
     if (int e = mark(0, s)) return e;
-    if (int e = herr(hipEventRecord(sc->fork, s))) return e;
-    for (int i = 0; i < na; ++i)
-        if (int e = herr(hipStreamWaitEvent(sc->aux[i], sc->fork, 0))) return e;
-    // pieced parts (sc->pieces > 1): chunk windows [wc[j], wc[j + 1]) — 0, 4, 16, 64, ...
-    // chunks, the last window open — block-passed on `s` window by window, both parts
-    // interleaved, each window's walk on the part's stream after its window's event
-    const int np = std::min(sc->pieces, LGCN_SCHED_MAX_PIECES);
-    auto pieced = [&](int i) {
-        return np > 1 && i < 2 && parts[i].r1 > parts[i].r0 && p.emu_part_max_blocks[i] > 0 &&
-               parts[i].r1 - parts[i].r0 <= 65535;
-    };
-    auto wchunk = [&](int j) { return j <= 0 ? 0 : j >= np ? INT32_MAX : 1 << (2 * j); };
-    auto wblock = [&](int i, int j) {  // first block of window j's chunks (block 0 in window 0)
-        const int64_t c = wchunk(j);
-        return (int32_t)std::min<int64_t>(c == 0 ? 0 : 1 + 64 * c, p.emu_part_max_blocks[i]);
-    };
+    hipEvent_t fork;
+    if (int e = record(sc, s, &fork)) return e;
+    for (int i = 0; i < na; ++i) {
+        const hipEvent_t w = own && i < 2 && dp->part_wait[i] ? dp->part_wait[i] : fork;
+        if (int e = wait_ev(sc->aux[i], w)) return e;
+    }
     // block passes first (the walk of part 0 starts as soon as its own is done), then the layer
     // kernel, then the walks and the chains
     for (int i = 0; i < 3; ++i)
-        if ((i < 2 || !chains) && !pieced(i)) {
+        if (i < 2 || !chains) {
             if (int e = part_blocks(edges, p, parts[i], x, xdiv, x_nz, d, nullptr, aux_of(i)))
                 return e;
             if (i < 2)
                 if (int e = mark(1 + i, aux_of(i))) return e;
         }
-    for (int j = 0; j < np; ++j)
-        for (int i = 0; i < 2; ++i) {
-            if (!pieced(i) || wblock(i, j) >= wblock(i, j + 1)) continue;
-            if (int e = lgcn_emu_blocks_rows(edges, p.emu_blocks, p.emu_rows + parts[i].r0,
-                                             parts[i].r1 - parts[i].r0, wblock(i, j),
-                                             wblock(i, j + 1), x, xdiv, x_nz, d, p.emu_rel,
-                                             p.emu_meta, p.emu_stage, nullptr, s))
-                return e;
-            if (int e = herr(hipEventRecord(sc->piece_ev[i][j], s))) return e;
-            if (wblock(i, j + 1) >= p.emu_part_max_blocks[i])
-                if (int e = mark(1 + i, s)) return e;
-        }
-    // the block passes read X only; every kernel after them writes Y, whose epilogue operands are
-    // ready once `late` fires
-    if (sc->late) {
-        if (int e = herr(hipStreamWaitEvent(s, sc->late, 0))) return e;
-        for (int i = 0; i < na; ++i)
-            if (int e = herr(hipStreamWaitEvent(sc->aux[i], sc->late, 0))) return e;
-    }
-    if (sc->blocks_first && sc->blocks_done && parts[0].b1 > parts[0].b0 && !pieced(0)) {
-        if (int e = herr(hipEventRecord(sc->blocks_done, aux_of(0)))) return e;
-        if (int e = herr(hipStreamWaitEvent(s, sc->blocks_done, 0))) return e;
-    }
-    // a layer that walks nothing (C3's user half-layers: a few short chain rows) runs its chains
-    // on `s` before the layer kernel (LGCN_SCHED_CHAINS_FIRST): launched on an aux stream they
-    // were dispatched only once the layer kernel's grid was (~3.5 ms at C3)
-    const bool chains_first = chains && sc->chains_first && parts[0].r1 == parts[0].r0 &&
-                              parts[1].r1 == parts[1].r0;
-    if (chains_first) {
-        if (int e = chain_rows(s)) return e;
-        if (int e = mark(4, s)) return e;
-    }
+    // the block passes read X only; every kernel after them writes Y, whose epilogue operands
+    // are ready once `late` fires
+    if (int e = wait_late(s, dp)) return e;
+    for (int i = 0; i < na; ++i)
+        if (int e = wait_late(sc->aux[i], dp)) return e;
+    // the layer kernel waits for part 0's block pass
+    if (parts[0].b1 > parts[0].b0)
+        if (int e = link(sc, aux_of(0), s)) return e;
     if (int e = layer_kernel(s)) return e;
     if (int e = mark(3, s)) return e;
-    if (chains && !chains_first) {
+    if (chains) {
         if (int e = chain_rows(aux_of(2))) return e;
         if (int e = mark(4, aux_of(2))) return e;
     }
     for (int i = 0; i < 3; ++i)
         if (i < 2 || !chains) {
-            if (pieced(i)) {
-                for (int j = 0; j < np && wblock(i, j) < wblock(i, j + 1); ++j) {
-                    if (int e = herr(hipStreamWaitEvent(aux_of(i), sc->piece_ev[i][j], 0)))
-                        return e;
-                    if (int e = lgcn_emu_walk_chunks(
-                            edges, p.emu_blocks, p.emu_rows + parts[i].r0,
-                            parts[i].r1 - parts[i].r0, p.emu_rel, p.emu_meta, p.emu_stage, x,
-                            xdiv, x_nz, y, ldy, d, &ep, slots[i], nullptr, wchunk(j),
-                            wchunk(j + 1), aux_of(i)))
-                        return e;
-                }
-            } else if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep,
-                                         slots[i], nullptr, aux_of(i))) {
+            if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
+                                  nullptr, aux_of(i)))
                 return e;
-            }
             if (i < 2)
                 if (int e = mark(5 + i, aux_of(i))) return e;
         }
-    // join: every row of Y written before `s` goes on
+    // join: every row of Y written before `s` goes on — except deferred parts 0 and 1
     for (int i = 0; i < na; ++i) {
-        if (int e = herr(hipEventRecord(sc->join[i], sc->aux[i]))) return e;
-        if (int e = herr(hipStreamWaitEvent(s, sc->join[i], 0))) return e;
+        if (own && dp->defer && i < 2) {
+            if (int e = record(sc, sc->aux[i], &dp->part_done[i])) return e;
+        } else if (int e = link(sc, sc->aux[i], s)) {
+            return e;
+        }
     }
-    return mark(7, s);
+    if (int e = mark(7, s)) return e;
+    return own ? 0 : done_on_s();
 }
-
-#ifdef LGCN_CAPTURE_DEBUG
-// capture-crash bisection (variant build): LGCN_CAPTURE_EXP bits — 1: lane 1's aux streams are
-// not forked from the caller's stream, 2: nor joined into it, 4: lane 0 keeps one aux stream,
-// 8: lane 1 keeps its aux streams under a capture
-int cap_exp() {
-    static const int v = getenv("LGCN_CAPTURE_EXP") ? atoi(getenv("LGCN_CAPTURE_EXP")) : 0;
-    return v;
-}
-#else
-constexpr int cap_exp() { return 0; }
-#endif
 
 // The bipartite schedule (lgcn_propagate_*_sides): a lane = the stream its half-layers' layer
 // kernels run on + the schedule view whose aux streams take their emulated / chain rows.
@@ -1127,34 +1208,6 @@ struct Lane {
     const lgcn_sched* view;
 };
 
-// Half-layer (k, side): the rows of slots [0, split) (side 0) or [split, n) (side 1), under that
-// side's plan with scratch set k & 1, traced at trace_sides[((k - 1) * 2 + side) * 8].
-int half_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
-               int32_t n, int32_t split, const lgcn_hub_plan_t* plans, int k, int side,
-               const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y, int32_t d,
-               const lgcn_epilogue_t& ep, const lgcn_sched* sc, const Lane& L,
-               hipEvent_t late = nullptr) {
-    const int32_t s0 = side ? split : 0, s1 = side ? n : split;
-    if (s1 <= s0) return 0;
-    const int h = (k - 1) * 2 + side;
-    lgcn_sched v;
-    const lgcn_sched* vp = nullptr;
-    hipEvent_t* tm = sc ? sc->timing_sides : nullptr;
-    if (L.view) {
-        v = *L.view;
-        v.t0 = tm ? tm[2 * h] : nullptr;
-        v.t1 = tm ? tm[2 * h + 1] : nullptr;
-        v.trace = sc && sc->trace_sides ? sc->trace_sides + h * 8 : nullptr;
-        v.late = late;
-        if ((cap_exp() & 4) && L.view == sc && v.n_aux > 1) v.n_aux = 1;
-        vp = &v;
-    } else if (late) {
-        if (int e = herr(hipStreamWaitEvent(L.main, late, 0))) return e;
-    }
-    return plan_layer(rowptr + s0, edges, row_ids + s0, s1 - s0, plans[2 * side + (k & 1)], x,
-                      xdiv, x_nz, y, d, d, ep, vp, L.main);
-}
-
 bool capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
@@ -1162,53 +1215,44 @@ bool capturing(hipStream_t s) {
 
 // The two lanes: lane 1 on its own streams when the schedule has them, else both lanes share
 // the caller's stream (half-layers then run in layer order, each still overlapped inside).
-// While `s` is being captured into a HIP graph, lane 1 runs its half-layers on its main stream
-// alone (parts in order): a capture that forks lane 1's own aux streams as well crashes
-// hipStreamEndCapture on this ROCm (segfault; the same lanes without them capture and replay
-// bitwise, tests/test_gpu_sides.py).
+// While `s` is being captured, lane 1 runs its half-layers on its main stream alone unless
+// LGCN_SCHED_CAPTURE_AUX = 1 (rounds 3-4: a capture that forked lane 1's own aux streams crashed
+// hipStreamEndCapture while one fork/join event was re-recorded across the half-layers of a
+// call; every record now has its own event).
 bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2], bool& l1_aux) {
     lanes[0] = Lane{s, sc};
     const bool two = sc && sc->lane1;
-    l1_aux = two && sc->lane1->n_aux > 0 && (!capturing(s) || (cap_exp() & 8));
+    const bool cap = capturing(s);
+    l1_aux = two && sc->lane1->n_aux > 0 && (!cap || sc->capture_aux);
     lanes[1] = two ? Lane{sc->lane1_main, l1_aux ? sc->lane1 : nullptr} : lanes[0];
+    if (sc) {
+        sc->pool->state[0] = two ? 2 : 1;
+        sc->pool->state[1] = l1_aux ? sc->lane1->n_aux : 0;
+        sc->pool->state[2] = cap ? 1 : 0;
+    }
     return two;
 }
 
-// Lane 1 forked from the caller's stream: its main stream AND its aux streams wait on `s` first
-// (a stream captured by way of another forked stream — origin -> A -> B — crashes HIP's
-// hipStreamEndCapture on this ROCm; every stream entering the capture from the origin is fine).
+// Lane 1 forked from the caller's stream: its main stream and its aux streams wait on `s`.
 int fork_lanes(const lgcn_sched* sc, bool two, bool l1_aux, hipStream_t s) {
     if (!two) return 0;
-    if (int e = herr(hipEventRecord(sc->lane_fork, s))) return e;
-    if (int e = herr(hipStreamWaitEvent(sc->lane1_main, sc->lane_fork, 0))) return e;
+    hipEvent_t f;
+    if (int e = record(sc, s, &f)) return e;
+    if (int e = wait_ev(sc->lane1_main, f)) return e;
     const lgcn_sched* l1 = sc->lane1;
-    for (int i = 0; i < (l1_aux && !(cap_exp() & 1) ? l1->n_aux : 0); ++i)
-        if (int e = herr(hipStreamWaitEvent(l1->aux[i], sc->lane_fork, 0))) return e;
+    for (int i = 0; i < (l1_aux ? l1->n_aux : 0); ++i)
+        if (int e = wait_ev(l1->aux[i], f)) return e;
     return 0;
 }
 
-// Lane 1 back into the caller's stream: its main stream and (already joined into that) its aux
-// streams, each also joined into `s` directly — a captured stream forked from another forked
-// stream must still end joined into the capture's origin for hipStreamEndCapture.
+// Lane 1 back into the caller's stream: its main stream and its aux streams, each joined into
+// `s` directly.
 int join_lanes(const lgcn_sched* sc, bool two, bool l1_aux, hipStream_t s) {
     if (!two) return 0;
-    if (int e = herr(hipEventRecord(sc->lane_join, sc->lane1_main))) return e;
-    if (int e = herr(hipStreamWaitEvent(s, sc->lane_join, 0))) return e;
+    if (int e = link(sc, sc->lane1_main, s)) return e;
     const lgcn_sched* l1 = sc->lane1;
-    for (int i = 0; i < (l1_aux && !(cap_exp() & 2) ? l1->n_aux : 0); ++i) {
-        if (int e = herr(hipEventRecord(l1->join[i], l1->aux[i]))) return e;
-        if (int e = herr(hipStreamWaitEvent(s, l1->join[i], 0))) return e;
-    }
-    return 0;
-}
-
-int check_plan(const lgcn_hub_plan_t* p);
-
-int check_sides(const int32_t* rowptr, const int32_t* row_ids, int32_t n, int32_t split,
-                const lgcn_hub_plan_t* plans) {
-    if (!plans || !rowptr || (n > 0 && !row_ids) || split < 0 || split > n) return LGCN_EINVAL;
-    for (int i = 0; i < 4; ++i)
-        if (int e = check_plan(plans + i)) return e;
+    for (int i = 0; i < (l1_aux ? l1->n_aux : 0); ++i)
+        if (int e = link(sc, l1->aux[i], s)) return e;
     return 0;
 }
 
@@ -1229,6 +1273,165 @@ int check_plan(const lgcn_hub_plan_t* p) {
     if (p->emu_scratch_blocks > 0 && (!p->emu_rel || !p->emu_meta)) return LGCN_EINVAL;
     return 0;
 }
+
+// segments of a sided propagation: 0..2 = the side-0 classes, 3 = side 1
+constexpr int kSegs = 4;
+
+int check_sides(const int32_t* rowptr, const int32_t* row_ids, int32_t n, const lgcn_sides_t* sd,
+                const lgcn_hub_plan_t* plans) {
+    if (!plans || !rowptr || !sd || (n > 0 && !row_ids)) return LGCN_EINVAL;
+    const int32_t c0 = sd->class_end[0], c1 = sd->class_end[1], sp = sd->split;
+    if (c0 < 0 || c0 > c1 || c1 > sp || sp > n) return LGCN_EINVAL;
+    if (sd->part_rows[0] < 0 || sd->part_rows[0] > sd->part_rows[1] ||
+        sd->part_rows[1] > n - sp)
+        return LGCN_EINVAL;
+    for (int i = 0; i < 2 * kSegs; ++i)
+        if (int e = check_plan(plans + i)) return e;
+    return 0;
+}
+
+// The classes hold when side 1's walked parts are covered by the rows they were built from:
+// plan part 0 = side-1 slots [split, split + emu_part_rows[0]) (a plan over a degree-ordered
+// slot range lists its emulated rows in slot order), part 1 up to emu_part_rows[1].
+bool classes_hold(const lgcn_sides_t& sd, const lgcn_hub_plan_t* plans) {
+    for (int j = 0; j < 2; ++j) {
+        const lgcn_hub_plan_t& p = plans[2 * 3 + j];
+        if (p.emu_part_rows[0] > sd.part_rows[0] || p.emu_part_rows[1] > sd.part_rows[1])
+            return false;
+    }
+    return true;
+}
+
+// What layer k of a sided propagation reads and writes.
+struct LayerIO {
+    lgcn_rows_t x;
+    float xdiv;
+    const uint32_t* x_nz;
+    float* y;
+    lgcn_epilogue_t ep;
+};
+
+// Segment g of layer k: slots [lo, hi) under plans[2 * g + (k & 1)] on lane L.
+int seg_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+              int32_t lo, int32_t hi, const lgcn_hub_plan_t* plans, int k, int g,
+              const LayerIO& io, int32_t d, const lgcn_sched* sc, const Lane& L, Deps* dp) {
+    if (hi <= lo) {  // nothing to run: the deferred parts are "done" here
+        if (dp && dp->defer && sc)
+            for (int i = 0; i < 2; ++i)
+                if (int e = record(sc, L.main, &dp->part_done[i])) return e;
+        return 0;
+    }
+    const int h = (k - 1) * kSegs + g;
+    lgcn_sched v;
+    const lgcn_sched* vp = nullptr;
+    if (L.view) {
+        v = *L.view;
+        v.t0 = sc->timing_sides ? sc->timing_sides[2 * h] : nullptr;
+        v.t1 = sc->timing_sides ? sc->timing_sides[2 * h + 1] : nullptr;
+        v.trace = sc->trace_sides ? sc->trace_sides + h * 8 : nullptr;
+        vp = &v;
+    }
+    Deps local;
+    Deps* dq = dp;
+    if (!vp && dp && dp->defer && sc) {
+        // (no view: everything runs on L.main; plan_layer records nothing without a schedule)
+        local = *dp;
+        local.defer = false;
+        dq = &local;
+    }
+    if (int e = plan_layer(rowptr + lo, edges, row_ids + lo, hi - lo, plans[2 * g + (k & 1)],
+                           io.x, io.xdiv, io.x_nz, io.y, d, d, io.ep, vp, L.main, dq))
+        return e;
+    if (dq == &local)
+        for (int i = 0; i < 2; ++i)
+            if (int e = record(sc, L.main, &dp->part_done[i])) return e;
+    return 0;
+}
+
+// The sided propagation (forward and backward): layer k of one side reads layer k-1 of the
+// other. Half-layer (k, side) runs on lane (k + side + K) % 2, so each lane is a chain of
+// half-layers that alternate sides, and layer k of one side follows layer k-1 of the other on
+// its own lane. Side 0 runs as its classes (class A = rows linked to side 1's walked part 0, B =
+// to part 1 only, C = the rest; lgcn_csr_side_classes), and the walked parts of side 1 wait
+// only for the classes they read:
+//  - layer 1 of side 0 runs A, B, C: layer 2's part 0 (the longest walk) starts once A is done;
+//  - side 1's parts 0 and 1 are not joined into their lane: layer k+1 of side 0 runs C (reads
+//    side 1's other rows), then B after part 1, then A after part 0, so the classes that do not
+//    read the longest walks run while it is still going;
+//  - a mean (forward, k = K) waits, per class / per part, only for the rows of layer K-1 it reads.
+// Backward buffers alternate (layer k overwrites layer k-2's rows): a part of side 1 overwrites
+// rows that only the classes it waited for read, and a class of side 0 overwrites rows that only
+// the parts it waited for read.
+int run_sides(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+              const lgcn_sides_t& sd, const lgcn_hub_plan_t* plans, int32_t d, int32_t K,
+              const std::function<LayerIO(int)>& layer, const lgcn_sched* sched, hipStream_t s) {
+    Lane lanes[2];
+    bool l1_aux = false;
+    if (sched) sched->pool->next = 0;
+    const bool two = make_lanes(sched, s, lanes, l1_aux);
+    // Under a HIP-graph capture the parts are joined into their lane at the end of every
+    // half-layer (no deferred parts, no early starts, no cross-lane waits on an aux stream): a
+    // capture with those crashed hipStreamEndCapture on this ROCm (round 5, in the first test
+    // that captured them); the captured graph keeps the per-class launches and the two lanes.
+    const bool cap = capturing(s);
+    const bool classes = sched && sched->classes && classes_hold(sd, plans) && !cap;
+    if (sched) sched->pool->state[3] = classes ? 1 : 0;
+    const int32_t lo[kSegs] = {0, sd.class_end[0], sd.class_end[1], sd.split};
+    const int32_t hi[kSegs] = {sd.class_end[0], sd.class_end[1], sd.split, 0};
+    auto seg_hi = [&](int g, int32_t n) { return g == 3 ? n : hi[g]; };
+    const int32_t n = sd.n;
+    if (int e = fork_lanes(sched, two, l1_aux, s)) return e;  // lane 1 starts where `s` is
+    constexpr int KM = LGCN_MAX_LAYERS + 2;
+    hipEvent_t cls[KM][3] = {}, ab[KM] = {}, rest[KM] = {}, part[KM][2] = {};
+    for (int k = 1; k <= K; ++k) {
+        const LayerIO io = layer(k);
+        const bool mean = io.ep.mode == LGCN_EPI_MEAN;
+        {  // side 1
+            const Lane& L = lanes[(k + 1 + K) & 1];
+            Deps dp;
+            if (classes && k >= 2) {
+                dp.part_wait[0] = cls[k - 1][0];
+                dp.part_wait[1] = ab[k - 1];
+            }
+            dp.defer = k < K && sched && !cap;
+            if (mean && k >= 2) {
+                dp.late[0] = rest[k - 1];
+                dp.late[1] = part[k - 1][0];
+                dp.late[2] = part[k - 1][1];
+            }
+            if (int e = seg_layer(rowptr, edges, row_ids, sd.split, n, plans, k, 3, io, d, sched,
+                                  L, &dp))
+                return e;
+            if (k < K && sched) {
+                if (int e = record(sched, L.main, &rest[k])) return e;
+                part[k][0] = dp.part_done[0];
+                part[k][1] = dp.part_done[1];
+            }
+        }
+        {  // side 0, one class at a time
+            const Lane& L = lanes[(k + K) & 1];
+            static const int up[3] = {0, 1, 2}, down[3] = {2, 1, 0};
+            const int* order = k == 1 ? up : down;
+            for (int t = 0; t < 3; ++t) {
+                const int c = order[t];
+                // (without classes every class reads everything: all wait for both parts)
+                if (k >= 2 && (c <= 1 || !classes))
+                    if (int e = wait_ev(L.main, part[k - 1][1])) return e;
+                if (k >= 2 && (c == 0 || !classes))
+                    if (int e = wait_ev(L.main, part[k - 1][0])) return e;
+                Deps dp;
+                if (mean && k >= 2) dp.late[0] = cls[k - 1][c];
+                if (int e = seg_layer(rowptr, edges, row_ids, lo[c], seg_hi(c, n), plans, k, c,
+                                      io, d, sched, L, &dp))
+                    return e;
+                if (sched)
+                    if (int e = record(sched, L.main, &cls[k][c])) return e;
+            }
+            ab[k] = k == 1 ? cls[k][1] : cls[k][0];
+        }
+    }
+    return join_lanes(sched, two, l1_aux, s);
+}
 }  // namespace
 
 extern "C" {
@@ -1238,37 +1441,38 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
     for (int i = 0; i < n_aux; ++i)
         if (!aux_streams[i]) return LGCN_EINVAL;
     lgcn_sched* sc = new (std::nothrow) lgcn_sched();
-    if (!sc) return LGCN_EINVAL;
+    EventPool* pool = new (std::nothrow) EventPool();
+    if (!sc || !pool) {
+        delete sc;
+        delete pool;
+        return LGCN_EINVAL;
+    }
     memset(sc, 0, sizeof(*sc));
+    sc->pool = pool;
     const int n0 = n_aux < 3 ? n_aux : 3;
     sc->n_aux = n0;
     sc->chain = 1;
+    sc->classes = 1;
+    sc->capture_aux = 0;
     for (int i = 0; i < n0; ++i) sc->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[i]);
-    auto mk = [](hipEvent_t* ev) { return herr(hipEventCreateWithFlags(ev, hipEventDisableTiming)); };
-    int e = mk(&sc->fork);
-    for (int i = 0; i < n0 && !e; ++i) e = mk(&sc->join[i]);
-    if (!e) e = mk(&sc->blocks_done);
-    for (int i = 0; i < 2 && !e; ++i)
-        for (int j = 0; j < LGCN_SCHED_MAX_PIECES && !e; ++j) e = mk(&sc->piece_ev[i][j]);
+    int e = 0;
+    for (; pool->n < kPoolEvents && !e; ++pool->n)
+        e = herr(hipEventCreateWithFlags(&pool->ev[pool->n], hipEventDisableTiming));
+    if (e) --pool->n;  // (the failed slot holds no event)
     if (!e && n_aux >= 4) {
         sc->lane1_main = reinterpret_cast<hipStream_t>(aux_streams[3]);
         sc->lane1 = new (std::nothrow) lgcn_sched();
         if (!sc->lane1) e = LGCN_EINVAL;
         if (!e) {
-            memset(sc->lane1, 0, sizeof(*sc->lane1));
             lgcn_sched* l1 = sc->lane1;
+            memset(l1, 0, sizeof(*l1));
+            l1->pool = pool;
             l1->n_aux = n_aux - 4;
             l1->chain = 1;
+            l1->classes = 1;
+            l1->capture_aux = 0;
             for (int i = 0; i < l1->n_aux; ++i)
                 l1->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[4 + i]);
-            e = mk(&l1->fork);
-            for (int i = 0; i < l1->n_aux && !e; ++i) e = mk(&l1->join[i]);
-            if (!e) e = mk(&l1->blocks_done);
-            for (int i = 0; i < 2 && !e; ++i)
-                for (int j = 0; j < LGCN_SCHED_MAX_PIECES && !e; ++j) e = mk(&l1->piece_ev[i][j]);
-            if (!e) e = mk(&sc->lane_fork);
-            if (!e) e = mk(&sc->lane_join);
-            for (int i = 0; i < 2 && !e; ++i) e = mk(&sc->cross[i]);
         }
     }
     if (e) {
@@ -1281,17 +1485,11 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
 
 int lgcn_sched_destroy(lgcn_sched_t* sc) {
     if (!sc) return 0;
-    if (sc->fork) (void)hipEventDestroy(sc->fork);
-    if (sc->blocks_done) (void)hipEventDestroy(sc->blocks_done);
-    for (int i = 0; i < 2; ++i)
-        for (int j = 0; j < LGCN_SCHED_MAX_PIECES; ++j)
-            if (sc->piece_ev[i][j]) (void)hipEventDestroy(sc->piece_ev[i][j]);
-    for (int i = 0; i < 3; ++i)
-        if (sc->join[i]) (void)hipEventDestroy(sc->join[i]);
-    hipEvent_t* own[] = {&sc->lane_fork, &sc->lane_join, &sc->cross[0], &sc->cross[1]};
-    for (hipEvent_t* ev : own)
-        if (*ev) (void)hipEventDestroy(*ev);
-    if (sc->lane1) lgcn_sched_destroy(sc->lane1);
+    if (sc->pool) {
+        for (int i = 0; i < sc->pool->n; ++i) (void)hipEventDestroy(sc->pool->ev[i]);
+        delete sc->pool;
+    }
+    delete sc->lane1;  // (a view: shares the root's pool)
     delete sc;
     return 0;
 }
@@ -1321,39 +1519,23 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
         case LGCN_SCHED_TRACE_SIDES:
             sc->trace_sides = reinterpret_cast<hipEvent_t*>(value);
             return 0;
-        case LGCN_SCHED_BLOCKS_FIRST:
-            sc->blocks_first = value != 0;
-            if (sc->lane1) sc->lane1->blocks_first = value != 0;
-            return 0;
-        case LGCN_SCHED_MEAN_EARLY:
-            sc->mean_early = value != 0;
-            return 0;
-        case LGCN_SCHED_PRESUM:
-            if (value < 0 || value > 3) return LGCN_EINVAL;
-            sc->presum = (int)value;
-            return 0;
-        case LGCN_SCHED_PRESUM_BUF:
-            sc->presum_buf = reinterpret_cast<float*>(value);
-            return 0;
-        case LGCN_SCHED_LANE_FLIP:
-            if (value < 0 || value > 3) return LGCN_EINVAL;
-            sc->lane_flip = (int)value;
-            return 0;
-        case LGCN_SCHED_CHAINS_FIRST:
-            sc->chains_first = value != 0;
-            if (sc->lane1) sc->lane1->chains_first = value != 0;
-            return 0;
-        case LGCN_SCHED_PIECES:
-            if (value < 0 || value > LGCN_SCHED_MAX_PIECES) return LGCN_EINVAL;
-            sc->pieces = (int)value;
-            if (sc->lane1) sc->lane1->pieces = (int)value;
-            return 0;
         case LGCN_SCHED_TIMING_SIDES:
             sc->timing_sides = reinterpret_cast<hipEvent_t*>(value);
+            return 0;
+        case LGCN_SCHED_CLASSES:
+            sc->classes = value != 0;
+            return 0;
+        case LGCN_SCHED_CAPTURE_AUX:
+            sc->capture_aux = value != 0;
             return 0;
         default:
             return LGCN_EINVAL;
     }
+}
+
+int64_t lgcn_sched_state(const lgcn_sched_t* sc, int32_t what) {
+    if (!sc || what < LGCN_SCHED_STATE_LANES || what > LGCN_SCHED_STATE_CLASSES) return LGCN_EINVAL;
+    return sc->pool->state[what - LGCN_SCHED_STATE_LANES];
 }
 
 int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
@@ -1366,6 +1548,7 @@ int lgcn_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     if (n_rows > 0 && (!rowptr || !y || ldy < d)) return LGCN_EINVAL;
     if (!(x_div > 0.f)) return LGCN_EINVAL;
     if (epi_host->mode != LGCN_EPI_ADD && (x_div != 1.f || x_nz)) return LGCN_EINVAL;
+    if (sched) sched->pool->next = 0;
     return plan_layer(rowptr, edges, row_ids, n_rows, *plan, x, x_div, x_nz, y, ldy, d,
                       *epi_host, sched, S(stream));
 }
@@ -1381,6 +1564,7 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
     hipStream_t s = S(stream);
     if (K == 0) return scale_rows(emb, n, d, 1.0f, out, d, s);
     if (int e = check_plan(plan)) return e;
+    if (sched) sched->pool->next = 0;
     for (int k = 1; k <= K; ++k) {
         const lgcn_rows_t x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
         lgcn_epilogue_t ep;
@@ -1412,121 +1596,67 @@ int lgcn_propagate_forward(const int32_t* rowptr, const lgcn_edge_t* edges,
 }
 
 int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
-                                 const int32_t* row_ids, int32_t n, int32_t split,
+                                 const int32_t* row_ids, const lgcn_sides_t* sides,
                                  const lgcn_hub_plan_t* plans, lgcn_rows_t emb, int32_t d,
                                  int32_t K, float* const* layer_bufs_host, float* out,
                                  const lgcn_sched_t* sched, void* stream) {
+    const int32_t n = sides ? sides->n : -1;
     if (int e = valid_geom(n, d)) return e;
     if (K < 0 || K - 1 > LGCN_MAX_LAYERS || !out) return K < 0 || !out ? LGCN_EINVAL : LGCN_ETOOMANY;
     if (K > 1 && !layer_bufs_host) return LGCN_EINVAL;
     hipStream_t s = S(stream);
     if (K == 0) return scale_rows(emb, n, d, 1.0f, out, d, s);
-    if (int e = check_sides(rowptr, row_ids, n, split, plans)) return e;
-    Lane lanes[2];
-    bool l1_aux = false;
-    const bool two = make_lanes(sched, s, lanes, l1_aux);
-    if (int e = fork_lanes(sched, two, l1_aux, s)) return e;  // lane 1 starts where `s` is (E0 ready)
-    for (int k = 1; k <= K; ++k) {
-        const lgcn_rows_t x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
-        lgcn_epilogue_t ep;
-        memset(&ep, 0, sizeof(ep));
-        float* y;
+    if (int e = check_sides(rowptr, row_ids, n, sides, plans)) return e;
+    auto layer = [&](int k) {
+        LayerIO io;
+        memset(&io, 0, sizeof(io));
+        io.x = (k == 1) ? emb : dense_rows(layer_bufs_host[k - 2], n, d);
+        io.xdiv = 1.f;
         if (k < K) {
-            ep.mode = LGCN_EPI_STORE;
-            y = layer_bufs_host[k - 1];
+            io.ep.mode = LGCN_EPI_STORE;
+            io.y = layer_bufs_host[k - 1];
         } else {
-            ep.mode = LGCN_EPI_MEAN;
-            ep.n_prev = K;
-            ep.div = (float)(K + 1);
-            ep.prev0 = emb;
-            for (int i = 0; i + 1 < K; ++i) ep.prev_dense[i] = layer_bufs_host[i];
-            ep.ld_prev = d;
-            y = out;
+            io.ep.mode = LGCN_EPI_MEAN;
+            io.ep.n_prev = K;
+            io.ep.div = (float)(K + 1);
+            io.ep.prev0 = emb;
+            for (int i = 0; i + 1 < K; ++i) io.ep.prev_dense[i] = layer_bufs_host[i];
+            io.ep.ld_prev = d;
+            io.y = out;
         }
-        // the item side first: its half-layer holds the longest walks (host submission order
-        // only; the two sides of one layer are independent)
-        for (int side = 1; side >= 0; --side) {
-            const Lane& L = lanes[(k + side + K + (sched && (sched->lane_flip & 1) ? 1 : 0)) & 1];
-            // PRESUM: the side's mean reads S = ((E0 + E1) + ...) + E_{K-1}, summed right after
-            // its layer K-1 (below) on that lane — one row read instead of K, same rounding
-            bool presum = two && K >= 2 && sched->presum_buf && ((sched->presum >> side) & 1) &&
-                          d % 4 == 0 && rows_aligned(emb) && al16(sched->presum_buf);
-            for (int i = 0; presum && i + 1 < K; ++i) presum = al16(layer_bufs_host[i]);
-            lgcn_epilogue_t eps = ep;
-            if (presum && k == K) {
-                eps.prev0 = dense_rows(sched->presum_buf, n, d);
-                eps.n_prev = 1;
-            }
-            // the mean of a side reads its layer K-1, computed on the other lane: the half-layer
-            // waits for it — or, with MEAN_EARLY, only its kernels that write Y do
-            hipEvent_t late = nullptr;
-            if (two && k == K && K >= 2) {
-                if (sched->mean_early)
-                    late = sched->cross[side];
-                else if (int e = herr(hipStreamWaitEvent(L.main, sched->cross[side], 0)))
-                    return e;
-            }
-            if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, x, 1.f,
-                                   nullptr, y, d, presum && k == K ? eps : ep, sched, L, late))
-                return e;
-            if (presum && k == K - 1) {
-                lgcn_epilogue_t pe;
-                memset(&pe, 0, sizeof(pe));
-                pe.prev0 = emb;
-                pe.n_prev = K;
-                for (int i = 0; i + 1 < K; ++i) pe.prev_dense[i] = layer_bufs_host[i];
-                pe.ld_prev = d;
-                const int32_t s0 = side ? split : 0, s1 = side ? n : split;
-                if (int e = presum_rows(row_ids + s0, s1 - s0, pe, d, sched->presum_buf, L.main))
-                    return e;
-            }
-            if (two && k == K - 1)
-                if (int e = herr(hipEventRecord(sched->cross[side], L.main))) return e;
-        }
-    }
-    return join_lanes(sched, two, l1_aux, s);
+        return io;
+    };
+    return run_sides(rowptr, edges, row_ids, *sides, plans, d, K, layer, sched, s);
 }
 
 int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
-                                  const int32_t* row_ids, int32_t n, int32_t split,
+                                  const int32_t* row_ids, const lgcn_sides_t* sides,
                                   const lgcn_hub_plan_t* plans, lgcn_rows_t grad_out,
                                   const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                                   float* grad_e0, const lgcn_sched_t* sched, void* stream) {
+    const int32_t n = sides ? sides->n : -1;
     if (int e = valid_geom(n, d)) return e;
     if (K < 0 || !grad_out.p0 || !grad_e0) return LGCN_EINVAL;
     hipStream_t s = S(stream);
     if (K == 0) return scale_rows(grad_out, n, d, 1.0f, grad_e0, d, s);
     if (K > 1 && !work_h) return LGCN_EINVAL;
-    if (int e = check_sides(rowptr, row_ids, n, split, plans)) return e;
-    Lane lanes[2];
-    bool l1_aux = false;
-    const bool two = make_lanes(sched, s, lanes, l1_aux);
-    if (int e = fork_lanes(sched, two, l1_aux, s)) return e;
-    // as lgcn_propagate_backward; half-layer (k, side) reads layer k-1's other side, written on
-    // the same lane, and overwrites (alternate buffers) layer k-2's same side, which only the
-    // same lane's half-layer (k-1, other side) read
-    const float div = (float)(K + 1);
-    lgcn_epilogue_t ep;
-    memset(&ep, 0, sizeof(ep));
-    ep.mode = LGCN_EPI_ADD;
-    ep.addend = grad_out;
-    ep.addend_nz = grad_nz;
-    ep.div = div;
-    lgcn_rows_t h = grad_out;
-    float xdiv = div;
-    const uint32_t* x_nz = grad_nz;
-    for (int k = 1; k <= K; ++k) {
-        float* y = ((K - k) % 2 == 0) ? grad_e0 : work_h;
-        for (int side = 1; side >= 0; --side)
-            if (int e = half_layer(rowptr, edges, row_ids, n, split, plans, k, side, h, xdiv, x_nz,
-                                   y, d, ep, sched,
-                                   lanes[(k + side + K + (sched && (sched->lane_flip & 2) ? 1 : 0)) & 1]))
-                return e;
-        h = dense_rows(y, n, d);
-        xdiv = 1.f;
-        x_nz = nullptr;
-    }
-    return join_lanes(sched, two, l1_aux, s);
+    if (int e = check_sides(rowptr, row_ids, n, sides, plans)) return e;
+    // as lgcn_propagate_backward: h = G/(K+1) + Âᵀ h, layer k into grad_e0 or work_h alternately
+    auto out_of = [&](int k) { return ((K - k) % 2 == 0) ? grad_e0 : work_h; };
+    auto layer = [&](int k) {
+        LayerIO io;
+        memset(&io, 0, sizeof(io));
+        io.x = k == 1 ? grad_out : dense_rows(out_of(k - 1), n, d);
+        io.xdiv = k == 1 ? (float)(K + 1) : 1.f;
+        io.x_nz = k == 1 ? grad_nz : nullptr;
+        io.y = out_of(k);
+        io.ep.mode = LGCN_EPI_ADD;
+        io.ep.addend = grad_out;
+        io.ep.addend_nz = grad_nz;
+        io.ep.div = (float)(K + 1);
+        return io;
+    };
+    return run_sides(rowptr, edges, row_ids, *sides, plans, d, K, layer, sched, s);
 }
 
 int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
@@ -1540,6 +1670,7 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
     if (K == 0) return scale_rows(grad_out, n, d, 1.0f, grad_e0, d, s);
     if (K > 1 && !work_h) return LGCN_EINVAL;
     if (int e = check_plan(plan)) return e;
+    if (sched) sched->pool->next = 0;
     // MeanBackward hands every layer c = G / (K+1); it is never materialised: layer 1 gathers
     // G / (K+1) on load and every epilogue adds G[row] / (K+1) (same rounding as c).
     const float div = (float)(K + 1);

@@ -45,7 +45,6 @@
 #include "lgcn.h"
 
 namespace lgcn_detail {
-extern int g_emu_resolve;  // LGCN_TUNE_EMU_RESOLVE (lgcn_engine.hip)
 extern int g_emu_margin;   // LGCN_TUNE_EMU_MARGIN (lgcn_engine.hip)
 }
 
@@ -122,10 +121,6 @@ __device__ __forceinline__ int lsb_exp_z(float f) {
     return (__float_as_uint(f) << 1) ? lsb_exp(f) : -100000;
 }
 
-// lowest-set-bit exponent of the exact product v * x (-100000: the product is zero)
-__device__ __forceinline__ int lsb_exp_prod(float v, float x) {
-    return (v != 0.f && x != 0.f) ? lsb_exp(v) + lsb_exp(x) : -100000;
-}
 
 // ---------------------------------------------------------------------------------------------
 // block pass: one wave per (block, 64-column slice); lane = column
@@ -146,9 +141,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
                                                    int4* __restrict__ ktab,
                                                    int4* __restrict__ meta,
                                                    float* __restrict__ stage,
-                                                   const lgcn_emu_row_t* __restrict__ live,
-                                                   const lgcn_emu_row_t* __restrict__ prows,
-                                                   int32_t k_lo, int32_t k_hi) {
+                                                   const lgcn_emu_row_t* __restrict__ live) {
     // steps gathered per sub-window (all in flight at once), two sub-windows in flight
 #ifndef LGCN_BLK_SW
 #define LGCN_BLK_SW 16
@@ -158,15 +151,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
     const int lane = threadIdx.x;
     const int c = blockIdx.y * 64 + lane;
     const bool act = c < d;
-    // the block: blockIdx.x, or (row window, lgcn_emu_blocks_rows) block k_lo + blockIdx.x of
-    // row prows[blockIdx.z] when the row has it
-    int64_t bi = blockIdx.x;
-    if (prows) {
-        const lgcn_emu_row_t pr = prows[blockIdx.z];
-        const int32_t k = k_lo + (int32_t)blockIdx.x;
-        if (k >= min(k_hi, pr.n_blocks)) return;
-        bi = pr.first_block + k;
-    }
+    const int64_t bi = blockIdx.x;
     const lgcn_emu_block_t blk = blocks[bi];
     // a row the live-edge chains run (lgcn_live_rows flags it) needs no block pass
     if (live && live[blk.row].n_blocks) return;
@@ -214,8 +199,17 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             *reinterpret_cast<float4*>(tp + 4 * q) =
                 make_float4(xv[4 * q], xv[4 * q + 1], xv[4 * q + 2], xv[4 * q + 3]);
     };
+    // the tile is written by each lane for its own column and read across lanes: a wave barrier
+    // with wavefront-scope release/acquire orders the LDS writes before the reads (and the reads
+    // before the next sub-window rewrites the tile) under the memory model, not only by issue order
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     auto stage_flush = [&](int step0) {  // the tile's 32 steps -> stage, 8 columns a store
         if (!staging) return;
+        wave_sync();
         const int sub = lane >> 3, q = lane & 7;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -225,6 +219,7 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             if (cg < d)
                 *reinterpret_cast<float4*>(st0 + (int64_t)cg * LGCN_EMU_BLOCK + step0 + 4 * q) = v;
         }
+        wave_sync();
     };
     // one sub-window: steps past the block end read as (0, 0), and fma(0, 0, c) == c for every
     // chain value (a chain is never -0), so the unrolled steps need no guard
@@ -515,101 +510,33 @@ __device__ __forceinline__ uint32_t seq_block(const float* __restrict__ sv,
 }
 
 // The resolution of one block: the sequential chain a = fma(v_j, x_j, a), j < n, over the
-// block's (val, x) pairs in an LDS slot (sv, sx), read once into registers (lane l: steps
-// 4l..4l+3). With max_it = 0 (the default) it is the chain itself (seq_reg). Otherwise up to
-// max_it runs of exact integer steps first (header comment): per run, every step's q_j in the
-// chain value's binade, a wave prefix sum, and the first step that could leave the binade or be
-// a tie is taken by the reference's fma, followed by a short sequential burst; the rest of the
-// block, once the runs are spent, is the sequential chain. Measured on the Books-scale graph,
-// a chain value next to a binade boundary crosses it many times in a row (~19 exits per resolved
-// block), so the runs do not pay there; they stay as a tunable (LGCN_TUNE_EMU_RESOLVE).
+// block's (val, x) pairs in an LDS slot (sv, sx): a whole block LGCN_SEQ_STEPS steps per lane
+// (seq_block), a shorter last block 4 steps per lane (seq_reg). (Round 3 measured parallel
+// runs of exact integer steps before the chain: a chain value next to a binade boundary crosses
+// it ~19 times per resolved block on the Books-scale graph, so they did not pay and are gone.)
 // Returns the bits of the value after the block.
 __device__ __forceinline__ uint32_t resolve_block(const float* __restrict__ sv,
-                                                  const float* __restrict__ sx, int n, uint32_t a,
-                                                  int max_it, unsigned long long* iters) {
-    constexpr int kBurst = 16;
+                                                  const float* __restrict__ sx, int n, uint32_t a) {
     const int lane = threadIdx.x;
-    // a whole block (every block of a row but possibly its last): LGCN_SEQ_STEPS per lane
-    if (max_it <= 0 && n == LGCN_EMU_BLOCK) return seq_block<LGCN_SEQ_STEPS>(sv, sx, a);
+    if (n == LGCN_EMU_BLOCK) return seq_block<LGCN_SEQ_STEPS>(sv, sx, a);
     const float4 v4 = *reinterpret_cast<const float4*>(sv + 4 * lane);
     const float4 x4 = *reinterpret_cast<const float4*>(sx + 4 * lane);
     const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
     const float xv[4] = {x4.x, x4.y, x4.z, x4.w};
-    if (max_it <= 0) return seq_reg(vv, xv, 0, n, a);
-    int le[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) le[k] = lsb_exp_prod(vv[k], xv[k]);
-    int j0 = 0;
-    for (int it = 0; j0 < n; ++it) {
-        if (it >= max_it) return seq_reg(vv, xv, j0, n, a);
-        if (iters) ++*iters;
-        const int E = (int)((a >> 23) & 255u);
-        if ((unsigned)(E - 1) >= 254u) {  // zero, subnormal, inf or NaN: the reference's steps
-            const int j1 = min(n, j0 + kBurst);
-            a = seq_reg(vv, xv, j0, j1, a);
-            j0 = j1;
-            continue;
-        }
-        const int e = E - 127;
-        const int neg = (int)(a >> 31);
-        const int M = (int)((a & 0x7fffffu) | 0x800000u);
-        const float C = __uint_as_float(((uint32_t)E << 23) | 0x400000u);  // 1.5 * 2^e
-        int q[4];
-        bool bad[4], on[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = 4 * lane + k;
-            on[k] = j >= j0 && j < n;
-            // |R - C| < 2^(e-2) keeps C + p inside binade e, so R - C = RN_u(p) exactly
-            const float R = __builtin_fmaf(vv[k], xv[k], C);
-            const float qf = ldexpf(R - C, 23 - e);
-            const bool big = !(fabsf(qf) < 2097152.f);  // >= 2^21 ulps, or NaN
-            bad[k] = on[k] && (big || le[k] >= e - 24);
-            q[k] = (on[k] && !big) ? (int)qf : 0;
-        }
-        const int c1 = q[0], c2 = c1 + q[1], c3 = c2 + q[2], c4 = c3 + q[3];
-        const int ex = wave_incl_scan(c4) - c4;
-        const int cs[4] = {ex + c1, ex + c2, ex + c3, ex + c4};  // prefix through step 4l + k
-        int fm = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int mag = neg ? M - cs[k] : M + cs[k];
-            // the exact result lies within 1/2 unit of mag: inside the binade for mag in
-            // [2^23 + 1, 2^24 - 1]
-            const bool f = bad[k] || (on[k] && (mag < (1 << 23) + 1 || mag > (1 << 24) - 1));
-            fm |= f ? (1 << k) : 0;
-        }
-        const unsigned long long lanes = __ballot(fm != 0);
-        if (!lanes) {
-            const int tot = __builtin_amdgcn_readlane(cs[3], 63);
-            return a + (uint32_t)(neg ? -tot : tot);
-        }
-        const int L = (int)__builtin_ctzll(lanes);
-        const int kf = __builtin_ctz((unsigned)__builtin_amdgcn_readlane(fm, L));
-        const int f = 4 * L + kf;
-        // the steps before f translate; from step f on, a sequential burst
-        const int pbl = kf == 0 ? ex : kf == 1 ? cs[0] : kf == 2 ? cs[1] : cs[2];
-        const int pb = __builtin_amdgcn_readlane(pbl, L);
-        const int j1 = min(n, f + kBurst);
-        a = seq_reg(vv, xv, f, j1, a + (uint32_t)(neg ? -pb : pb));
-        j0 = j1;
-    }
-    return a;
+    return seq_reg(vv, xv, 0, n, a);
 }
 
-template <int MODE, int XD, bool ISO>
+template <int MODE, int XD>
 __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__ edges,
                                                  const lgcn_emu_block_t* __restrict__ blocks,
                                                  const lgcn_emu_row_t* __restrict__ rows,
                                                  const int4* __restrict__ ktab,
-                                                 int4* __restrict__ meta,
+                                                 const int4* __restrict__ meta,
                                                  const float* __restrict__ stage, lgcn_rows_t x,
                                                  float xdiv, const uint32_t* __restrict__ x_nz,
                                                  int32_t d, float* __restrict__ y, int64_t ldy,
-                                                 lgcn_epilogue_t ep, int NS, int max_it,
-                                                 int pmargin,
-                                                 const lgcn_emu_row_t* __restrict__ live,
-                                                 int32_t ch_lo, int32_t ch_hi) {
+                                                 lgcn_epilogue_t ep, int NS, int pmargin,
+                                                 const lgcn_emu_row_t* __restrict__ live) {
     constexpr int CH = LGCN_EMU_CH;
     constexpr int B = LGCN_EMU_BLOCK;
     static_assert(CH == 64, "one lane per block of a chunk");
@@ -624,9 +551,6 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // issue priority over the co-resident waves of other kernels on this SIMD (build flag A/B)
     __builtin_amdgcn_s_setprio(LGCN_WALK_PRIO);
 #endif
-    // ISO: the wave holds the SIMD's whole register file (v255 and a255 claimed), so no other
-    // wave shares its issue slots — the walk is issue-bound on one wave
-    if constexpr (ISO) asm volatile("" ::: "v255", "a255");
     // a row the live-edge chains run (lgcn_live_rows flags it, aligned with `rows`) is theirs
     if (live && live[blockIdx.x].n_blocks) return;
     const lgcn_emu_row_t er = rows[blockIdx.x];
@@ -635,27 +559,19 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // block k of the row holds edges [row_beg + k * B, min(.. + B, row_end)) (plan_emulation)
     const int32_t row_beg = blocks[fb].beg;
     const int32_t row_end = blocks[fb + nb_all - 1].end;
-    // chunks of blocks 1, 2, ...; this launch walks chunks [ch_lo, ch_end) (a chunk window:
-    // lgcn_emu_walk_chunks), a row with none of them left has been written
-    const int nch_all = (nb_all - 1 + CH - 1) / CH;
-    if (ch_lo > 0 && nch_all <= ch_lo) return;
-    const int nch = min(nch_all, ch_hi);
-    // the chain value as its bits (wave-uniform): block 0's chain from +0 is the true chain; its
-    // meta word w also carries the value from one chunk window to the next (written below, read
-    // here: block 0's record is read by nothing else)
-    int* const carry = reinterpret_cast<int*>(meta + fb * d + c) + 3;
-    uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(*carry);
+    // chunks of blocks 1, 2, ... (64 blocks each)
+    const int nch = (nb_all - 1 + CH - 1) / CH;
+    constexpr int ch_lo = 0;
+    // the chain value as its bits (wave-uniform): block 0's chain from +0 is the true chain
+    uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(meta[fb * d + c].w);
     const bool staged = stage != nullptr;
     const int spare = 2 * NS;
 #ifdef LGCN_EMU_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long n_fast = 0, n_slow = 0, t_slow = 0, n_iter = 0;
+    unsigned long long n_fast = 0, n_slow = 0, t_slow = 0;
     unsigned long long ph[16] = {0};
     unsigned long long est[8] = {0};
     unsigned long long ph_last = t_start;
-    unsigned long long* iters = &n_iter;
-#else
-    unsigned long long* iters = nullptr;
 #endif
     struct Tab {
         int4 m;
@@ -908,7 +824,7 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
 #if defined(LGCN_EMU_STATS) || defined(LGCN_EMU_MODES)
                 if (g_emu_mode != 1 && g_emu_mode < 4)
 #endif
-                    ab = resolve_block(s_dyn + sl, s_dyn + sl + B, n, ab, max_it, iters);
+                    ab = resolve_block(s_dyn + sl, s_dyn + sl + B, n, ab);
                 PH_MARK(4);
                 PH_COUNT(10, 1);
 #ifdef LGCN_EMU_STATS
@@ -949,8 +865,6 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA lands after the wave is gone
 #ifdef LGCN_EMU_STATS
-    ph[12] = n_iter;
-    est[4] += n_iter;
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
         for (int k = 0; k < 16; ++k) g_emu_phase[k] += ph[k];
     if (lane == 0)
@@ -963,10 +877,6 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     }
 #endif
     if (lane != 0) return;
-    if (nch < nch_all) {  // chunks left for a later window: carry the chain value there
-        *carry = (int)ab;
-        return;
-    }
     const int32_t row = er.row;
     float out = __uint_as_float(ab);
     if constexpr (MODE == LGCN_EPI_MEAN) {
@@ -991,25 +901,23 @@ bool is_pow2(float x) {
     return x > 0.f && frexpf(x, &e) == 0.5f;
 }
 
-// n_blocks blocks from `blocks`; or (prows) blocks [k_lo, k_hi) of rows prows[0 .. n_blocks)
+// n_blocks blocks from `blocks`
 template <int XD>
 int launch_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
                   const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, int32_t d, int4* ktab,
-                  int4* meta, float* stage, const lgcn_emu_row_t* live, hipStream_t s,
-                  const lgcn_emu_row_t* prows = nullptr, int32_t k_lo = 0, int32_t k_hi = 0) {
-    const dim3 grid(prows ? (uint32_t)(k_hi - k_lo) : (uint32_t)n_blocks, (uint32_t)((d + 63) / 64),
-                    prows ? (uint32_t)n_blocks : 1u);
+                  int4* meta, float* stage, const lgcn_emu_row_t* live, hipStream_t s) {
+    const dim3 grid((uint32_t)n_blocks, (uint32_t)((d + 63) / 64));
     hipLaunchKernelGGL((k_emu_blocks<XD>), grid, dim3(64), 0, s, edges, blocks, x, xdiv, x_nz, d,
-                       ktab, meta, stage, live, prows, k_lo, k_hi);
+                       ktab, meta, stage, live);
     return herr_x(hipGetLastError());
 }
 
 template <int MODE, int XD>
 int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, int4* meta,
+                const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
                 const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
                 int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
-                const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi, hipStream_t s) {
+                const lgcn_emu_row_t* live, hipStream_t s) {
     const dim3 grid((uint32_t)n_rows, (uint32_t)d);
     const size_t lds = (size_t)(2 * slots + 1) * 2 * LGCN_EMU_BLOCK * sizeof(float);
     if (lds > 56 * 1024) {
@@ -1020,28 +928,16 @@ int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         if (hipError_t e = hipGetDevice(&dev)) return (int)e;
         const uint64_t bit = dev < 64 ? (1ull << dev) : 0;
         if (!bit || !(raised.load(std::memory_order_relaxed) & bit)) {
-            for (const void* f : {reinterpret_cast<const void*>(&k_emu_walk<MODE, XD, false>),
-                                  reinterpret_cast<const void*>(&k_emu_walk<MODE, XD, true>)}) {
-                const hipError_t e = hipFuncSetAttribute(
-                    f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
-                if (e != hipSuccess) return (int)e;
-            }
+            const hipError_t e = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&k_emu_walk<MODE, XD>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
+            if (e != hipSuccess) return (int)e;
             raised.fetch_or(bit, std::memory_order_relaxed);
         }
     }
-#ifndef LGCN_WALK_ISO_SLOTS
-#define LGCN_WALK_ISO_SLOTS 1000  // (build-time A/B: walks of this many slots or more isolated)
-#endif
-    if (slots >= LGCN_WALK_ISO_SLOTS)
-        hipLaunchKernelGGL((k_emu_walk<MODE, XD, true>), grid, dim3(64), lds, s, edges, blocks,
-                           rows, ktab, meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
-                           lgcn_detail::g_emu_resolve,
-                           lgcn_detail::g_emu_margin, live, ch_lo, ch_hi);
-    else
-        hipLaunchKernelGGL((k_emu_walk<MODE, XD, false>), grid, dim3(64), lds, s, edges, blocks,
-                           rows, ktab, meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
-                           lgcn_detail::g_emu_resolve,
-                           lgcn_detail::g_emu_margin, live, ch_lo, ch_hi);
+    hipLaunchKernelGGL((k_emu_walk<MODE, XD>), grid, dim3(64), lds, s, edges, blocks, rows, ktab,
+                       meta, stage, x, xdiv, x_nz, d, y, ldy, ep, slots,
+                       lgcn_detail::g_emu_margin, live);
     return herr_x(hipGetLastError());
 }
 
@@ -1051,12 +947,12 @@ int xd_of(float xdiv, const uint32_t* x_nz) {
 
 template <int MODE>
 int walk_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-              const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, int4* meta,
+              const lgcn_emu_row_t* rows, int32_t n_rows, const int4* ktab, const int4* meta,
               const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
               int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
-              const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi, hipStream_t s) {
+              const lgcn_emu_row_t* live, hipStream_t s) {
 #define LGCN_W(XD_) \
-    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
+    case XD_: return launch_walk<MODE, XD_>(edges, blocks, rows, n_rows, ktab, meta, stage, x, xdiv, x_nz, y, ldy, d, ep, slots, live, s);
     switch (xd) {
         LGCN_W(0) LGCN_W(1) LGCN_W(2) LGCN_W(4) LGCN_W(5) LGCN_W(6)
         default: return LGCN_EINVAL;
@@ -1480,38 +1376,11 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
 #undef LGCN_B
 }
 
-int lgcn_emu_blocks_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                         const lgcn_emu_row_t* rows, int32_t n_rows, int32_t k_lo, int32_t k_hi,
-                         lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
-                         void* meta, float* stage, const lgcn_emu_row_t* live, void* stream) {
-    if (n_rows < 0 || n_rows > 65535 || k_lo < 0 || d < 1 || d > 2048 || !(x_div > 0.f))
-        return LGCN_EINVAL;
-    if (n_rows == 0 || k_hi <= k_lo) return 0;
-    if (!edges || !blocks || !rows || !rel || !meta || !x.p0) return LGCN_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(rel) & 15) || (reinterpret_cast<uintptr_t>(meta) & 15) ||
-        (reinterpret_cast<uintptr_t>(stage) & 15))
-        return LGCN_EALIGN;
-    const int xd = xd_of(x_div, x_nz);
-    const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    int4* mp = static_cast<int4*>(meta);
-    int4* kp = reinterpret_cast<int4*>(rel);
-#define LGCN_B(XD_) \
-    case XD_: return launch_blocks<XD_>(edges, blocks, n_rows, x, xa, x_nz, d, kp, mp, stage, live, s, rows, k_lo, k_hi);
-    switch (xd) {
-        LGCN_B(0) LGCN_B(1) LGCN_B(2) LGCN_B(4) LGCN_B(5) LGCN_B(6)
-        default: return LGCN_EINVAL;
-    }
-#undef LGCN_B
-}
-
-int lgcn_emu_walk_chunks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                         const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, void* meta,
-                         const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz,
-                         float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
-                         int32_t slots, const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi,
-                         void* stream) {
-    if (ch_lo < 0 || ch_hi <= ch_lo) return LGCN_EINVAL;
+int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
+                  const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
+                  const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
+                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
+                  const lgcn_emu_row_t* live, void* stream) {
     if (slots == 0) slots = LGCN_EMU_SLOTS;
     // static LDS (two translation tables, 8 KB) + (2 slots + 1) x 2 KB within 64 KB
     if (n_rows < 0 || d < 1 || d > 2048 || !(x_div > 0.f) || !epi_host || slots < 1 ||
@@ -1537,31 +1406,19 @@ int lgcn_emu_walk_chunks(const lgcn_edge_t* edges, const lgcn_emu_block_t* block
     const int xd = xd_of(x_div, x_nz);
     const float xa = (xd & 3) == 2 ? 1.0f / x_div : x_div;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    int4* mp = static_cast<int4*>(meta);
+    const int4* mp = static_cast<const int4*>(meta);
     const int4* kp = reinterpret_cast<const int4*>(rel);
     switch (ep.mode) {
         case LGCN_EPI_STORE:
-            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
+            return walk_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         case LGCN_EPI_MEAN:
-            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
+            return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         case LGCN_EPI_ADD:
-            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, ch_lo, ch_hi, s);
+            return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         default:
             return LGCN_EINVAL;
     }
 }
-
-int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                  const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, const void* meta,
-                  const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
-                  int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
-                  const lgcn_emu_row_t* live, void* stream) {
-    // every chunk in one window: meta is only read
-    return lgcn_emu_walk_chunks(edges, blocks, rows, n_rows, rel, const_cast<void*>(meta), stage,
-                                x, x_div, x_nz, y, ldy, d, epi_host, slots, live, 0, INT32_MAX,
-                                stream);
-}
-
 
 int lgcn_chain_supported(int32_t d) { return d > 0 && d <= 2048 && d % 8 == 0; }
 

@@ -20,7 +20,6 @@ extern int g_rows_per_group;
 extern int g_unroll;
 extern int g_mean_prefetch;  // LGCN_TUNE_MEAN_PREFETCH: 2 = off
 extern int g_min_groups;     // LGCN_TUNE_MIN_GROUPS: 0 = 65536
-extern int g_emu_resolve;    // LGCN_TUNE_EMU_RESOLVE: parallel runs per resolved block
 
 // one lgcn_spmm_layer launch, geometry already chosen (dW = d / lanes' element width)
 struct LayerArgs {

@@ -24,17 +24,18 @@ LGCN_MAX_LAYERS = 16
 COO_ROWS_UNSORTED, COO_OUT_OF_RANGE, COO_COLS_UNSORTED = 1, 2, 4
 INT32_MAX = 2 ** 31 - 1
 TUNE_ROWS_PER_GROUP, TUNE_UNROLL, TUNE_MEAN_PREFETCH, TUNE_MIN_GROUPS = 1, 2, 3, 4
-TUNE_EMU_RESOLVE = 5
 TUNE_EMU_MARGIN = 6
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
-SCHED_TRACE_SIDES, SCHED_TIMING_SIDES, SCHED_BLOCKS_FIRST, SCHED_MEAN_EARLY = 7, 8, 9, 10
-SCHED_PIECES, SCHED_CHAINS_FIRST, SCHED_LANE_FLIP = 11, 12, 13
-SCHED_PRESUM, SCHED_PRESUM_BUF = 14, 15
+SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
+SCHED_CLASSES, SCHED_CAPTURE_AUX = 16, 17
+SCHED_STATE_LANES, SCHED_STATE_L1_AUX, SCHED_STATE_CAPTURING, SCHED_STATE_CLASSES = 1, 2, 3, 4
+# segments of a sided propagation: the three side-0 classes, then side 1
+N_SEGS = 4
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
-ABI_VERSION = 12
+ABI_VERSION = 13
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -132,6 +133,12 @@ class PlanT(ctypes.Structure):
                 ("emu_part_max_blocks", ctypes.c_int32 * 2)]
 
 
+class SidesT(ctypes.Structure):
+    """lgcn_sides_t"""
+    _fields_ = [("n", ctypes.c_int32), ("split", ctypes.c_int32), ("class_end", ctypes.c_int32 * 2),
+                ("part_rows", ctypes.c_int32 * 2)]
+
+
 class LgcnError(RuntimeError):
     pass
 
@@ -156,6 +163,8 @@ ABI = [
                                                 _P]),
     ("lgcn_csr_check_bipartite", ctypes.c_int, [_P, _P, _P, _I32, _I64, _I32, _I32, _P, _P]),
     ("lgcn_csr_relabel_cols", ctypes.c_int, [_P, _I64, _P, _P, _P]),
+    ("lgcn_csr_side_classes", ctypes.c_int, [_P, _P, _P, _I32, _I64, _I32, _I32, _I32, _P, _P, _P,
+                                             _P, _P, _P, ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lgcn_adj_degree", ctypes.c_int, [_P, _I64, _I32, _P, _P]),  # (sorted keys, ...)
     ("lgcn_adj_sort_unique", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
                                             ctypes.POINTER(ctypes.c_size_t), _P]),
@@ -180,11 +189,6 @@ ABI = [
                                        _P, _P]),
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
                                      _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P, _P]),
-    ("lgcn_emu_blocks_rows", ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, RowsT, ctypes.c_float,
-                                            _P, _I32, _P, _P, _P, _P, _P]),
-    ("lgcn_emu_walk_chunks", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float,
-                                            _P, _P, _I64, _I32, ctypes.POINTER(EpilogueT), _I32,
-                                            _P, _I32, _I32, _P]),
     ("lgcn_chain_supported", ctypes.c_int, [_I32]),
     ("lgcn_live_scratch_bytes", ctypes.c_size_t, [_I32, _I32]),
     ("lgcn_live_rows", ctypes.c_int, [_P, _P, _I32, _P, _I32, RowsT, ctypes.c_float, _P, _P, _I64,
@@ -195,16 +199,19 @@ ABI = [
     ("lgcn_sched_create", ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_void_p)]),
     ("lgcn_sched_destroy", ctypes.c_int, [_P]),
     ("lgcn_sched_set", ctypes.c_int, [_P, _I32, _I64]),
+    ("lgcn_sched_state", ctypes.c_int64, [_P, _I32]),
     ("lgcn_layer", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, ctypes.c_float, _P,
                                   _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P, _P]),
     ("lgcn_propagate_forward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _I32,
                                               _I32, _P, _P, _P, _P, _P]),
     ("lgcn_propagate_backward", ctypes.c_int, [_P, _P, _P, _I32, ctypes.POINTER(PlanT), RowsT, _P,
                                                _I32, _I32, _P, _P, _P, _P]),
-    ("lgcn_propagate_forward_sides", ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.POINTER(PlanT),
-                                                    RowsT, _I32, _I32, _P, _P, _P, _P]),
-    ("lgcn_propagate_backward_sides", ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.POINTER(PlanT),
-                                                     RowsT, _P, _I32, _I32, _P, _P, _P, _P]),
+    ("lgcn_propagate_forward_sides", ctypes.c_int, [_P, _P, _P, ctypes.POINTER(SidesT),
+                                                    ctypes.POINTER(PlanT), RowsT, _I32, _I32, _P,
+                                                    _P, _P, _P]),
+    ("lgcn_propagate_backward_sides", ctypes.c_int, [_P, _P, _P, ctypes.POINTER(SidesT),
+                                                     ctypes.POINTER(PlanT), RowsT, _P, _I32, _I32,
+                                                     _P, _P, _P, _P]),
 ]
 
 
@@ -229,9 +236,6 @@ def load_library(path=None):
         # LGCN_MEAN_PREFETCH=off: A/B switch of the MEAN layer's bundle prefetch (same bits)
         if os.environ.get("LGCN_MEAN_PREFETCH", "").lower() in ("0", "off"):
             lib.lgcn_tune(TUNE_MEAN_PREFETCH, 2)
-        # LGCN_EMU_RESOLVE=k: A/B switch of the walk's parallel runs per resolved block (same bits)
-        if os.environ.get("LGCN_EMU_RESOLVE", ""):
-            lib.lgcn_tune(TUNE_EMU_RESOLVE, int(os.environ["LGCN_EMU_RESOLVE"]))
         # LGCN_EMU_MARGIN=shift:base: A/B of the walk's prediction margin (same bits)
         if os.environ.get("LGCN_EMU_MARGIN", ""):
             sh, base = (int(t) for t in os.environ["LGCN_EMU_MARGIN"].split(":"))
@@ -391,8 +395,7 @@ class HubPlan:
         """(part_rows, part_blocks): the emulated rows cut into part 0 (rows of more than
         LGCN_EMU_PART0 = 8192 blocks, the longest walks: the layer's critical path), part 1 (more
         than chain_max_degree blocks) and the chain rows (lgcn_hub_plan_t emu_part_*)."""
-        b1 = -(-chain_max_degree(nnz) // LGCN_EMU_BLOCK)
-        b0 = max(int(os.environ.get("LGCN_EMU_PART0", "8192")), b1)
+        b0, b1 = walk_cut_blocks(nnz)
         nb = self.emu_nb
         cum = np.concatenate([[0], np.cumsum(nb)])
         r0, r1 = int((nb > b0).sum()), int((nb > b1).sum())
@@ -570,6 +573,10 @@ class Graph:
         # slots [split, n), every other row in [0, split) — the two half-layers of a layer
         self.sides = None
         self.split = None
+        # side-0 classes (lgcn_csr_side_classes): class ends and the side-1 part rows they were
+        # built from; (split, split) and (0, 0) without classes
+        self.class_end = None
+        self.class_parts = (0, 0)
         self._plans = {}
         self._rowptr_host = None
         self._row_ids_host = None
@@ -601,10 +608,24 @@ class Graph:
                                          self.row_ids_host(), mode=mode, emu_min=emu_min)
         return self._plans[key]
 
+    def segments(self):
+        """Slot ranges of the sided propagation's segments: side 0's three classes, side 1."""
+        ce = self.class_end or (self.split, self.split)
+        return [(0, ce[0]), (ce[0], ce[1]), (ce[1], self.split), (self.split, self.n_rows)]
+
+    def sides_struct(self):
+        """lgcn_sides_t of this side-major graph."""
+        ce = self.class_end or (self.split, self.split)
+        st = SidesT()
+        st.n, st.split = self.n_rows, self.split
+        st.class_end[0], st.class_end[1] = ce
+        st.part_rows[0], st.part_rows[1] = self.class_parts
+        return st
+
     def side_hubs(self, threshold, chunk=None, mode=None, emu_min=None):
-        """The hub plans (cached) of the two sides of a side-major graph: side 0 = slots
-        [0, split), side 1 = [split, n) — each over its slot range, row ids and edge offsets
-        absolute, as lgcn_propagate_*_sides takes them."""
+        """The hub plans (cached) of the segments of a side-major graph (segments(): side 0's
+        classes, then side 1) — each over its slot range, row ids and edge offsets absolute, as
+        lgcn_propagate_*_sides takes them."""
         if self.split is None:
             raise LgcnError("side_hubs needs a side-ordered graph (graph_from_coo(adj, sides=...))")
         mode = mode or hub_mode_from_env()
@@ -616,11 +637,10 @@ class Graph:
             ((chunk, DEFAULT_HUB_PRE_GROUP) if mode == "chunk" else (emu_min,))
         if key not in self._plans:
             rp, ids = self.rowptr_host(), self.row_ids_host()
-            sp = self.split
             self._plans[key] = [
                 plan_hubs(rp[a:b + 1], threshold, chunk, self.device, ids[a:b], mode=mode,
                           emu_min=emu_min)
-                for a, b in ((0, sp), (sp, self.n_rows))]
+                for a, b in self.segments()]
         return self._plans[key]
 
     def degrees(self):
@@ -671,6 +691,60 @@ def order_by_degree(lib, g, stream, sides=None):
     o.symmetric = g.symmetric
     if lo < hi:
         o.sides, o.split = (lo, hi), n - (hi - lo)
+        if classes_enabled():
+            o = side_classes(lib, o, stream)
+    return o
+
+
+def classes_enabled():
+    """Side-0 classes of a side-major slot order (LGCN_CLASSES=1; off by default: side 0 is then
+    one class and every walked part of side 1 waits for all of it; same bits). Measured at C3
+    (round 5): forward 14.4 ms with the classes vs 13.1-13.2 ms without — the users' first layer
+    as three launches ran 6.9 ms instead of 3.7 under the concurrent item work, which delayed
+    the items' layer 2 more than the early start of its longest walk gained."""
+    return os.environ.get("LGCN_CLASSES", "0") == "1"
+
+
+def walk_cut_blocks(nnz):
+    """(b0, b1): the emulated rows of more than b0 blocks are part 0 (LGCN_EMU_PART0, 8192),
+    of more than b1 = chain cut / LGCN_EMU_BLOCK part 1 (walked); the rest run as chains."""
+    b1 = -(-chain_max_degree(nnz) // LGCN_EMU_BLOCK)
+    return max(int(os.environ.get("LGCN_EMU_PART0", "8192")), b1), b1
+
+
+def side_classes(lib, g, stream):
+    """The side-major graph g with side 0's slots re-sorted by class (lgcn_csr_side_classes):
+    class 0 = rows linked to side 1's walked part 0 (its longest rows), 1 = to part 1 only, 2 =
+    the rest, each class in its degree order. The sided propagation then lets a walked part start
+    as soon as the classes it reads are done. Bitwise-neutral."""
+    n, nnz, dev, sp = g.n_rows, g.nnz, g.device, g.split
+    b0, b1 = walk_cut_blocks(nnz)
+    deg1 = np.diff(g.rowptr_host()[sp:].astype(np.int64))     # side 1, degree-descending
+    nb = -(-deg1 // LGCN_EMU_BLOCK)
+    p0, p01 = int((nb > b0).sum()), int((nb > b1).sum())
+    if p01 == 0 or sp == 0:
+        g.class_end, g.class_parts = (sp, sp), (0, 0)
+        return g
+    i32 = dict(dtype=torch.int32, device=dev)
+    work = torch.empty(5 * n, **i32)
+    row_ids = torch.empty(n, **i32)
+    rowptr = torch.empty(n + 1, **i32)
+    edges = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+    ce = torch.empty(2, **i32)
+    nbytes = ctypes.c_size_t(0)
+    args = (_ptr(g.rowptr), _ptr(g.edges), _ptr(g.row_ids), n, nnz, sp, p0, p01, _ptr(work),
+            _ptr(row_ids), _ptr(rowptr), _ptr(edges), _ptr(ce))
+    _check(lib.lgcn_csr_side_classes(*args, None, ctypes.byref(nbytes), stream),
+           "lgcn_csr_side_classes(size)")
+    temp = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
+    _check(lib.lgcn_csr_side_classes(*args, _ptr(temp), ctypes.byref(nbytes), stream),
+           "lgcn_csr_side_classes")
+    del work, temp
+    o = Graph(n, g.n_cols, rowptr, edges, nnz, dev, row_ids=row_ids)
+    o.symmetric = g.symmetric
+    o.sides, o.split = g.sides, sp
+    o.class_end = tuple(int(x) for x in ce.cpu().tolist())
+    o.class_parts = (p0, p01)
     return o
 
 
@@ -737,6 +811,7 @@ def relabel_slots(g):
     o.symmetric = g.symmetric
     if g.split is not None:  # side-major slots stay side-major: the sided schedule needs row ids
         o.sides, o.split = g.sides, g.split
+        o.class_end, o.class_parts = g.class_end, g.class_parts
         o.row_ids = torch.arange(g.n_rows, dtype=torch.int32, device=dev)
         o._row_ids_host = np.arange(g.n_rows, dtype=np.int32)
     return o, perm
@@ -890,11 +965,16 @@ def _stream_priorities(n_aux):
     rows' walks (a layer's critical path). Two lanes: all of lane 1 (aux 3 = its main stream and
     aux 4..6) — it carries the chain of half-layers ending in layer K's items, the propagation's
     critical path (lgcn_propagate_*_sides); LGCN_LANE_PRIORITY=part0 instead raises each lane's
-    part-0 stream (aux 0 and 4)."""
+    part-0 stream (aux 0 and 4), =parts both lanes' walked parts (aux 0, 1, 4, 5: the latency-bound
+    block passes and walks), leaving the layer kernels and chains of both lanes at normal
+    priority (4 + 4 streams: one hardware queue each under HIP's default)."""
     if n_aux <= 3:
         return [i == 0 for i in range(n_aux)]
-    if os.environ.get("LGCN_LANE_PRIORITY", "lane1") == "part0":
+    mode = os.environ.get("LGCN_LANE_PRIORITY", "lane1")
+    if mode == "part0":
         return [i in (0, 4) for i in range(n_aux)]
+    if mode == "parts":
+        return [i in (0, 1, 4, 5) for i in range(n_aux)]
     return [i >= 3 for i in range(n_aux)]
 
 
@@ -937,21 +1017,14 @@ class Sched:
         self.set(SCHED_SLOTS0, slots[0])
         self.set(SCHED_SLOTS1, slots[min(1, len(slots) - 1)])
         self.set(SCHED_CHAIN, 1 if chain_enabled() else 0)
-        # each layer kernel waits for its part 0 block pass, so the longest rows' walk starts
-        # before the layer kernel fills the chip (C3 forward 18.58 -> 18.06 ms; LGCN_BLOCKS_FIRST=0
-        # starts them together)
-        self.set(SCHED_BLOCKS_FIRST, 0 if os.environ.get("LGCN_BLOCKS_FIRST", "1") == "0" else 1)
-        # the final half-layer of a side forks its block passes before waiting for the other
-        # lane's layer K-1 (they read X only; LGCN_MEAN_EARLY=0: the whole half-layer waits)
-        self.set(SCHED_MEAN_EARLY, 0 if os.environ.get("LGCN_MEAN_EARLY", "1") == "0" else 1)
-        # LGCN_PIECES=2..4: parts 0 and 1 pipeline block pass and walk in chunk windows (A/B at
-        # C3: 14.23 vs 14.07 ms whole — the walk's first chunks are its slowest, and the
-        # windows' block passes share its SIMDs)
-        self.set(SCHED_PIECES, sched_pieces())
-        # LGCN_CHAINS_FIRST=1: a half-layer without walks (C3's users) runs its chain rows before
-        # its layer kernel (A/B: 13.7 ms best case at C3 but bimodal under the lane priorities)
-        self.set(SCHED_CHAINS_FIRST, 1 if os.environ.get("LGCN_CHAINS_FIRST", "0") == "1" else 0)
-        self.set(SCHED_LANE_FLIP, int(os.environ.get("LGCN_LANE_FLIP", "0") or 0))
+        # LGCN_SCHED_CLASSES=0: the walked parts of side 1 wait for the whole side-0 half-layer
+        # (A/B; same bits); LGCN_CAPTURE_AUX=1: lane 1 keeps its aux streams under a capture
+        self.set(SCHED_CLASSES, 0 if os.environ.get("LGCN_SCHED_CLASSES", "1") == "0" else 1)
+        self.set(SCHED_CAPTURE_AUX, 1 if os.environ.get("LGCN_CAPTURE_AUX", "0") == "1" else 0)
+
+    def state(self, what):
+        """lgcn_sched_state: what the latest sided call on this schedule ran."""
+        return int(self.lib.lgcn_sched_state(self.handle, what))
 
     def set(self, knob, value):
         _check(self.lib.lgcn_sched_set(self.handle, knob, int(value)), "lgcn_sched_set")
@@ -964,47 +1037,18 @@ class Sched:
             pass
 
 
-def _capture_aux(device):
-    """Auxiliary streams while the caller's stream is being captured into a HIP graph: the same
-    as eager (LGCN_CAPTURE_AUX overrides, for A/B). The C library keeps a capture safe itself:
-    under a capture lane 1 runs its half-layers on its main stream alone (lgcn_engine.hip
-    make_lanes — forking lane 1's own aux streams inside a capture crashes hipStreamEndCapture
-    on this ROCm), so a captured sided propagation still runs two lanes, same kernels and bits."""
-    if torch.cuda.is_current_stream_capturing():
-        cap = os.environ.get("LGCN_CAPTURE_AUX", "")
-        return min(int(cap), n_aux_streams()) if cap else n_aux_streams()
-    return None
-
-
 def sched_for(device, n_aux=None):
     """The device's Sched (None with LGCN_EMU_OVERLAP=0: every part in order on the caller's
-    stream). n_aux: default n_aux_streams()."""
+    stream). n_aux: default n_aux_streams(). Made outside any capture on first use (the C
+    library creates its events there; a captured call reuses them)."""
     if not emu_overlap_enabled():
         return None
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_BLOCKS_FIRST", ""),
-           os.environ.get("LGCN_MEAN_EARLY", ""), os.environ.get("LGCN_PIECES", ""),
-           os.environ.get("LGCN_CHAINS_FIRST", ""), os.environ.get("LGCN_LANE_FLIP", ""))
+           os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_SCHED_CLASSES", ""),
+           os.environ.get("LGCN_CAPTURE_AUX", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
-        if key[1] > 3:  # the one-lane schedule a capture falls back to, made outside any capture
-            sched_for(device, 3)
     return _scheds[key]
-
-
-def presum_sides():
-    """Sides whose final mean reads a pre-summed row (LGCN_PRESUM, bit s = side s; default 0 =
-    off: at C3 the users' presum (10.5 GB right after their layer 2) slows the items' layer 2,
-    the critical path, more than it saves in layer 3: forward 12.78 -> 13.3 ms with bit 0)."""
-    v = os.environ.get("LGCN_PRESUM", "0")
-    return max(0, min(3, int(v))) if v.strip() else 0
-
-
-def sched_pieces():
-    """Chunk windows of the pipelined block pass + walk of parts 0 and 1 (LGCN_PIECES, 0..4;
-    0/1 = each part's block pass, then its walk)."""
-    v = os.environ.get("LGCN_PIECES", "0")
-    return max(0, min(4, int(v))) if v.strip() else 0
 
 
 def chain_enabled():
@@ -1098,16 +1142,17 @@ def live_enabled():
 
 
 def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=False):
-    """The 4 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * side + set]. live: attach the
-    live-edge scratch (the backward of a row-sparse G)."""
+    """The 8 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * segment + set] (segments: the
+    side-0 classes, side 1). live: attach the live-edge scratch (the backward of a row-sparse
+    G)."""
     lib = load_library()
     hps = graph.side_hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
     chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and xs_aligned
-    arr = (PlanT * 4)()
-    for side in (0, 1):
+    arr = (PlanT * (2 * N_SEGS))()
+    for g in range(N_SEGS):
         for j in (0, 1):
-            arr[2 * side + j] = hps[side].struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
-                                                 scratch_set=j, live=live and live_enabled())
+            arr[2 * g + j] = hps[g].struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
+                                           scratch_set=j, live=live and live_enabled())
     return arr, hps
 
 
@@ -1122,10 +1167,10 @@ class _SideEvents:
         if sc is None:
             return
         if timing:
-            self.timing = [torch.cuda.Event(enable_timing=True) for _ in range(4 * K)]
+            self.timing = [torch.cuda.Event(enable_timing=True) for _ in range(2 * N_SEGS * K)]
             self._set(SCHED_TIMING_SIDES, self.timing)
         if trace:
-            self.trace = [torch.cuda.Event(enable_timing=True) for _ in range(16 * K)]
+            self.trace = [torch.cuda.Event(enable_timing=True) for _ in range(8 * N_SEGS * K)]
             self._set(SCHED_TRACE_SIDES, self.trace)
 
     def _set(self, knob, evs):
@@ -1141,19 +1186,26 @@ class _SideEvents:
             self.sc.set(SCHED_TRACE_SIDES, 0)
 
 
-side_trace = None   # a list: the sided entry points append {(k, side): [(phase, event)]} per call
-side_timing = None  # a list: ... append {(k, side): (start, end)} around each half-layer kernel
+side_trace = None   # a list: the sided entry points append {(k, g): [(phase, event)]} per call
+side_timing = None  # a list: ... append {(k, g): (start, end)} around each segment's layer kernel
+# (g: segment — 0..2 the side-0 classes, 3 side 1; empty segments are left out)
 
 
 last_schedule = None  # the schedule of the latest propagation call (diagnostics, tests)
 
 
-def _note_schedule(sc, sided):
+def _note_schedule(sc, graph):
+    """last_schedule from what the C library ran (lgcn_sched_state)."""
     global last_schedule
-    n = sc.n_aux if sc is not None else 0
-    # captured: lane 1 runs on its main stream alone (the C library's capture rule, make_lanes)
-    last_schedule = {"sided": sided, "aux_streams": n, "lanes": 2 if sided and n >= 4 else 1,
-                     "captured": torch.cuda.is_current_stream_capturing()}
+    if sc is None:
+        last_schedule = {"sided": True, "aux_streams": 0, "lanes": 1, "lane1_aux": 0,
+                         "captured": torch.cuda.is_current_stream_capturing(), "classes": False}
+        return
+    last_schedule = {"sided": True, "aux_streams": sc.n_aux,
+                     "lanes": sc.state(SCHED_STATE_LANES),
+                     "lane1_aux": sc.state(SCHED_STATE_L1_AUX),
+                     "captured": bool(sc.state(SCHED_STATE_CAPTURING)),
+                     "classes": bool(sc.state(SCHED_STATE_CLASSES))}
 
 
 def use_sides(graph, layer_events=None, kernel_events=None):
@@ -1162,15 +1214,17 @@ def use_sides(graph, layer_events=None, kernel_events=None):
     return graph.split is not None and layer_events is None and kernel_events is None
 
 
-def _collect_sides(ev, K):
+def _collect_sides(ev, K, graph):
+    segs = [g for g, (a, b) in enumerate(graph.segments()) if b > a]
     if ev.timing is not None and side_timing is not None:
-        side_timing.append({(k, s): (ev.timing[((k - 1) * 2 + s) * 2],
-                                     ev.timing[((k - 1) * 2 + s) * 2 + 1])
-                            for k in range(1, K + 1) for s in (0, 1)})
+        side_timing.append({(k, g): (ev.timing[((k - 1) * N_SEGS + g) * 2],
+                                     ev.timing[((k - 1) * N_SEGS + g) * 2 + 1])
+                            for k in range(1, K + 1) for g in segs})
     if ev.trace is not None and side_trace is not None:
-        side_trace.append({(k, s): list(zip(TRACE_PHASES, ev.trace[((k - 1) * 2 + s) * 8:
-                                                                    ((k - 1) * 2 + s + 1) * 8]))
-                           for k in range(1, K + 1) for s in (0, 1)})
+        side_trace.append({(k, g): list(zip(TRACE_PHASES,
+                                            ev.trace[((k - 1) * N_SEGS + g) * 8:
+                                                     ((k - 1) * N_SEGS + g + 1) * 8]))
+                           for k in range(1, K + 1) for g in segs})
 
 
 def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
@@ -1205,27 +1259,19 @@ def propagate_forward(graph, segments, K, hub_threshold=None, layer_events=None,
         if use_sides(graph, layer_events, kernel_events):
             plans, _ = _side_plans(graph, d, hub_threshold, hub_mode, emu_min,
                                    _aligned16(segments))
-            sc = sched_for(dev, _capture_aux(dev))
-            _note_schedule(sc, True)
+            sc = sched_for(dev)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             bufs = (ctypes.c_void_p * max(K - 1, 1))(*[t.data_ptr() for t in layers])
-            presum = None
-            if sc is not None:
-                # the users' mean reads one pre-summed row (LGCN_SCHED_PRESUM); the buffer lives
-                # until the lanes are joined back into `stream` (lgcn_propagate_forward_sides)
-                mask = presum_sides() if K >= 2 else 0
-                if mask:
-                    presum = torch.empty((n, d), dtype=torch.float32, device=dev)
-                sc.set(SCHED_PRESUM, mask)
-                sc.set(SCHED_PRESUM_BUF, presum.data_ptr() if presum is not None else 0)
+            sides = graph.sides_struct()
             try:
                 _check(lib.lgcn_propagate_forward_sides(
-                    _ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), n, graph.split,
-                    plans, e0, d, K, bufs, _ptr(out), sc.handle if sc is not None else None,
-                    stream), "lgcn_propagate_forward_sides")
+                    _ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids),
+                    ctypes.byref(sides), plans, e0, d, K, bufs, _ptr(out),
+                    sc.handle if sc is not None else None, stream), "lgcn_propagate_forward_sides")
             finally:
                 ev.clear()
-            _collect_sides(ev, K)
+            _note_schedule(sc, graph)
+            _collect_sides(ev, K, graph)
             return (out, layers) if return_layers else out
         hp = graph.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         for k in range(1, K + 1):
@@ -1309,18 +1355,19 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         if use_sides(gt):
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
                                    live=nz is not None)
-            sc = sched_for(dev, _capture_aux(dev))
-            _note_schedule(sc, True)
+            sc = sched_for(dev)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
+            sides = gt.sides_struct()
             try:
                 _check(lib.lgcn_propagate_backward_sides(
-                    _ptr(gt.rowptr), _ptr(gt.edges), _ptr(gt.row_ids), n, gt.split, plans, g,
-                    _ptr(nz), d, K, _ptr(work), _ptr(out),
+                    _ptr(gt.rowptr), _ptr(gt.edges), _ptr(gt.row_ids), ctypes.byref(sides),
+                    plans, g, _ptr(nz), d, K, _ptr(work), _ptr(out),
                     sc.handle if sc is not None else None, stream),
                     "lgcn_propagate_backward_sides")
             finally:
                 ev.clear()
-            _collect_sides(ev, K)
+            _note_schedule(sc, gt)
+            _collect_sides(ev, K, gt)
             return out
         hp = gt.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         ep = _epilogue(LGCN_EPI_ADD, addend=g, div=float(K + 1))

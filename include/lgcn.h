@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 12
+#define LGCN_ABI_VERSION 13
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
@@ -165,9 +165,8 @@ typedef struct {
      * 256-B aligned: with a row-sparse X (x_nz) every emulated row runs as a chain over its live
      * edges (lgcn_live_rows) instead of block pass + walk / chain over all of them */
     void* emu_live;
-    /* the longest row's block count in part 0 / part 1 (lgcn_plan_exact writes them); with
-     * LGCN_SCHED_PIECES the layer pipelines a part's block pass and walk in chunk windows up to
-     * it. 0 = unknown: that part runs whole */
+    /* the longest row's block count in part 0 / part 1 (lgcn_plan_exact writes them;
+     * informational) */
     int32_t emu_part_max_blocks[2];
 } lgcn_hub_plan_t;
 
@@ -223,9 +222,8 @@ const char* lgcn_error_string(int code);
                                        2 = off) */
 #define LGCN_TUNE_MIN_GROUPS     4  /* row bundles only when n_rows >= 2 x this many lane groups
                                        (0 = auto = 65536; 1 forces bundles on small graphs) */
-#define LGCN_TUNE_EMU_RESOLVE    5  /* emulation walk: parallel exact-step runs per block it must
-                                       resolve before the rest runs as the sequential chain
-                                       (default 0: always the sequential chain) */
+/* (5: LGCN_TUNE_EMU_RESOLVE until ABI 12 — the walk's parallel exact-step runs, measured slower
+   than the sequential chain and removed) */
 #define LGCN_TUNE_EMU_MARGIN     6  /* emulation walk: the prediction's widened bounds, base << 4 |
                                        shift: (hi - lo) >> shift + base (default 128 << 4 | 4;
                                        A/B at C3: 3,256 / 2,256 / 3,1024 / 2,2048 within noise);
@@ -299,6 +297,23 @@ int lgcn_csr_check_bipartite(const int32_t* rowptr, const lgcn_edge_t* edges,
  * their parameters there), so writes and the layer buffers are sequential. */
 int lgcn_csr_relabel_cols(const lgcn_edge_t* edges, int64_t nnz, const int32_t* new_id,
                           lgcn_edge_t* edges_out, void* stream);
+
+/* Side-0 classes of a side-major slot order (lgcn_csr_order_by_degree with sides; split = the
+ * first side-1 slot) for the sided propagation's dependency schedule: side-1 slots [split, split +
+ * part_rows0) are the rows of the side-1 plans' walked part 0 (the longest item rows), [split +
+ * part_rows0, split + part_rows1) part 1 — a degree-ordered plan lists its emulated rows in slot
+ * order, so these are the first slots of side 1. A side-0 row is class 0 if it is linked to a
+ * part-0 row, class 1 if linked to a part-1 row only, class 2 otherwise. Writes the same operator
+ * with side 0's slots stably re-sorted by class (each class keeps its degree order; side 1 is
+ * unchanged): row_ids_out / rowptr_out / edges_out as lgcn_csr_order_by_degree's, and
+ * class_end[0..1] (device int32[2]) = the first slot of class 1 and of class 2. Bitwise-neutral
+ * (every row keeps its edges). work: 5 n_rows int32 scratch. Two-call protocol for temp. Pass
+ * the class ends and part_rows to the sided propagation in lgcn_sides_t. */
+int lgcn_csr_side_classes(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* row_ids,
+                          int32_t n_rows, int64_t nnz, int32_t split, int32_t part_rows0,
+                          int32_t part_rows1, int32_t* work, int32_t* row_ids_out,
+                          int32_t* rowptr_out, lgcn_edge_t* edges_out, int32_t* class_end,
+                          void* temp, size_t* temp_bytes_host, void* stream);
 
 /* ---- adjacency builder (main.py:313-336 on the device) -------------------------------------- */
 /* deg[r] = number of stored edges with row r (duplicates counted, main.py:326 rowsum of the
@@ -381,28 +396,6 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
                   const lgcn_emu_row_t* live, void* stream);
 
-/* The block pass and the walk in chunk windows, so a walk can start before the whole block pass
- * is done (lgcn_layer pipelines them this way, LGCN_SCHED_PIECES). A row's block k > 0 lies in
- * chunk (k - 1) / 64 (block 0 starts the chain).
- * lgcn_emu_blocks_rows: the block pass of blocks [k_lo, k_hi) of each of rows[0 .. n_rows)
- * (n_rows <= 65535; blocks / rel / meta / stage indexed by the rows' first_block, the whole
- * arrays as for lgcn_emu_walk).
- * lgcn_emu_walk_chunks: lgcn_emu_walk over chunks [ch_lo, ch_hi) of every row. The first
- * window (ch_lo = 0) starts from block 0's chain; a row with chunks past ch_hi leaves its chain
- * value in block 0's meta record (so meta is written) for the next window, which starts from it;
- * the window holding a row's last chunk writes its Y row. Windows of one row run in order, each
- * after the block pass of its chunks (and block 0 before the first). */
-int lgcn_emu_blocks_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                         const lgcn_emu_row_t* rows, int32_t n_rows, int32_t k_lo, int32_t k_hi,
-                         lgcn_rows_t x, float x_div, const uint32_t* x_nz, int32_t d, float* rel,
-                         void* meta, float* stage, const lgcn_emu_row_t* live, void* stream);
-int lgcn_emu_walk_chunks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
-                         const lgcn_emu_row_t* rows, int32_t n_rows, const float* rel, void* meta,
-                         const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz,
-                         float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
-                         int32_t slots, const lgcn_emu_row_t* live, int32_t ch_lo, int32_t ch_hi,
-                         void* stream);
-
 /* Mid-size emulated rows run as the reference's sequential chain itself (no block pass): one
  * wave per (row, column slice) folds acc = fma(val_j, X[col_j, c], acc) in stored order from +0
  * while the next windows of gathered X rows are in flight by LDS-DMA. rows / blocks: as for
@@ -462,46 +455,29 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
 #define LGCN_SCHED_TRACE         6  /* hipEvent_t[8] (or 0): per-layer phase events — fork, part 0
                                        and part 1 block passes done, layer kernel done, chains
                                        done, part 0 and part 1 walks done, joined */
-#define LGCN_SCHED_TRACE_SIDES   7  /* hipEvent_t[16 * K] (or 0): the same 8 phases of every
-                                       half-layer of lgcn_propagate_*_sides, half-layer (k, side)
-                                       at [((k - 1) * 2 + side) * 8] */
-#define LGCN_SCHED_TIMING_SIDES  8  /* hipEvent_t[4 * K] (or 0): recorded on its lane's stream right
-                                       before / after the layer kernel of half-layer (k, side), at
-                                       [((k - 1) * 2 + side) * 2] and [... + 1] (timing) */
-#define LGCN_SCHED_BLOCKS_FIRST  9  /* 1: a layer kernel waits for its part 0 block pass (the
-                                       longest rows' walk then starts before the layer kernel
-                                       fills the chip; engine.py sets it); 0 (the C default):
-                                       they start together */
-#define LGCN_SCHED_MEAN_EARLY   10  /* 1: lgcn_propagate_forward_sides' final (mean) half-layer of a
-                                       side forks its block passes before it waits for that side's
-                                       layer K-1 on the other lane (they read X only); its layer
-                                       kernel, walks and chains wait (engine.py sets it); 0 (the
-                                       C default): the whole half-layer waits */
-#define LGCN_SCHED_PIECES       11  /* 2..4: parts 0 and 1 pipeline their block pass and walk in
-                                       that many chunk windows (0-3, 4-15, 16-63, 64+ chunks; the
-                                       last open): the block pass windows run on the caller's
-                                       stream before the layer kernel, the walk of a window starts
-                                       once its own block pass is done (lgcn_emu_blocks_rows /
-                                       lgcn_emu_walk_chunks; needs the plan's
-                                       emu_part_max_blocks). 0, 1 (the C default): whole parts */
-#define LGCN_SCHED_CHAINS_FIRST 12  /* 1: a layer that walks no rows (parts 0 and 1 empty) runs its
-                                       chain rows on the caller's stream before the layer kernel
-                                       (beside it on an aux stream they are dispatched only once
-                                       the layer kernel's grid is); 0 (the C default): beside */
-#define LGCN_SCHED_LANE_FLIP    13  /* bit 1 (forward) / bit 2 (backward): lgcn_propagate_*_sides
-                                       runs half-layer (k, side) on lane (k + side + K + 1) % 2 —
-                                       lane 1 (the high-priority streams) then carries the chain
-                                       ending in layer K's side 0; 0 (the C default):
-                                       (k + side + K) % 2 */
-#define LGCN_SCHED_PRESUM       14  /* bit s: lgcn_propagate_forward_sides writes side s's rows of
-                                       S = ((E0 + E1) + ...) + E_{K-1} into the PRESUM_BUF buffer
-                                       right after its layer K-1 (on that lane, before the other
-                                       lane's mean half-layer is released), and side s's mean
-                                       then reads S (one row instead of K; same rounding). Needs
-                                       the two lanes, K >= 2, d % 4 == 0, 16-B aligned E0 segments
-                                       and buffers; 0 (the C default): off */
-#define LGCN_SCHED_PRESUM_BUF   15  /* float* [n x d] (row ids, ld = d) for LGCN_SCHED_PRESUM */
+#define LGCN_SCHED_TRACE_SIDES   7  /* hipEvent_t[32 * K] (or 0): the same 8 phases of every
+                                       segment of lgcn_propagate_*_sides — g = 0..2 the side-0
+                                       classes, 3 side 1 — of layer k at [((k - 1) * 4 + g) * 8]
+                                       (an empty segment records none) */
+#define LGCN_SCHED_TIMING_SIDES  8  /* hipEvent_t[8 * K] (or 0): recorded on its lane's stream right
+                                       before / after the layer kernel of segment g of layer k,
+                                       at [((k - 1) * 4 + g) * 2] and [... + 1] (timing) */
+/* (9 .. 15: BLOCKS_FIRST and MEAN_EARLY — now always on — and the measured-and-dropped PIECES,
+   CHAINS_FIRST, LANE_FLIP, PRESUM, PRESUM_BUF of ABI 12) */
+#define LGCN_SCHED_CLASSES      16  /* 1 (default): lgcn_propagate_*_sides runs side 0 class by class
+                                       and lets side 1's walked parts wait only for the classes
+                                       they read (lgcn_sides_t); 0: every part waits for the
+                                       whole side-0 half-layer before it (same bits) */
+#define LGCN_SCHED_CAPTURE_AUX  17  /* 1: lane 1 keeps its aux streams while the caller's stream
+                                       is being captured into a HIP graph; 0 (default): lane 1 runs
+                                       its half-layers on its main stream alone under a capture */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
+/* What the latest lgcn_propagate_*_sides call on this schedule ran (diagnostics, tests). */
+#define LGCN_SCHED_STATE_LANES     1  /* 2: two lanes, 1: one */
+#define LGCN_SCHED_STATE_L1_AUX    2  /* aux streams lane 1 ran its parts on (0: its main stream) */
+#define LGCN_SCHED_STATE_CAPTURING 3  /* 1: the caller's stream was being captured */
+#define LGCN_SCHED_STATE_CLASSES   4  /* 1: the class dependencies were used */
+int64_t lgcn_sched_state(const lgcn_sched_t* sched, int32_t what);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +
  * chunk combine, the emulation block pass + walk of the emulated parts, the chain rows — every
@@ -535,27 +511,41 @@ int lgcn_propagate_backward(const int32_t* rowptr, const lgcn_edge_t* edges,
 
 /* Bipartite propagation: the rows of one side reference only rows of the other (users and
  * brands vs items, lgcn_csr_check_bipartite), so layer k of one side needs only layer k-1 of the
- * other. Every layer runs as two half-layers — slots [0, split) and [split, n) of a side-major
- * slot order (lgcn_csr_order_by_degree with side_lo < side_hi; split = its first slot of the
- * range side) — on two lanes: half-layer (k, side) on lane (k + side + K) % 2, each lane a chain
- * of half-layers that alternate sides; lane 1 (aux_streams[3..]) carries the chain that ends in
- * layer K's side-1 half-layer (the items': the longest rows), so its streams are the ones to
- * create at high priority. The longest rows' walks of one layer then overlap those of
- * the next instead of queueing behind them. Same arguments and results (bitwise) as
- * lgcn_propagate_forward / _backward, except:
- *  - plans: 4 hub plans, plans[2 * side + j]: side's plan (built over its slot range, row ids
- *    absolute) with two scratch sets j = 0, 1 (the half-layers of one side on consecutive layers
- *    run on different lanes, concurrently with each other);
+ * other. Every layer runs as half-layers over a side-major slot order (lgcn_csr_order_by_degree
+ * with side_lo < side_hi, then lgcn_csr_side_classes): side 0 = slots [0, split) in its three
+ * classes, side 1 = [split, n). Half-layer (k, side) runs on lane (k + side + K) % 2, each lane a
+ * chain of half-layers that alternate sides (lane 1 = aux_streams[3..]), and:
+ *  - layer 1 of side 0 runs class 0, 1, 2 in that order; the walked part 0 of layer 2's side 1
+ *    (the longest item rows: the critical path) starts once class 0 — the rows it reads — is
+ *    done, part 1 once classes 0 and 1 are;
+ *  - side 1's parts 0 and 1 are not joined into their lane: layer k+1 of side 0 runs class 2 (it
+ *    reads neither), then class 1 after part 1, then class 0 after part 0;
+ *  - a final mean half-layer waits, per class / part, for the rows of layer K-1 it reads (made
+ *    on the other lane), and its block passes not at all.
+ * Same arguments and results (bitwise) as lgcn_propagate_forward / _backward, except:
+ *  - sides: the slot layout (below); class_end = {split, split} and part_rows = {0, 0} when the
+ *    slot order has no classes (side 0 is then one class);
+ *  - plans: 8 hub plans, plans[2 * g + j] for segment g (0..2 = the side-0 classes, 3 = side 1;
+ *    each built over its slot range, row ids absolute) with two scratch sets j = 0, 1 (the
+ *    half-layers of one side on consecutive layers run on different lanes);
  *  - row_ids is required; no per-layer timing events (LGCN_SCHED_TRACE_SIDES traces phases);
- *  - forward: the final (mean) half-layer of a side also waits for that side's layer K-1 on the
- *    other lane (the mean reads it). */
+ *  - the class dependencies are used only when side 1's plans walk no rows outside the ones the
+ *    classes were built from (their emu_part_rows <= part_rows); otherwise every part waits for
+ *    the whole side-0 half-layer (lgcn_sched_state reports which). */
+typedef struct {
+    int32_t n;             /* rows (= slots) */
+    int32_t split;         /* first slot of side 1 */
+    int32_t class_end[2];  /* side 0: class 0 = [0, class_end[0]), 1 = [.., class_end[1]), 2 = the
+                              rest up to split (lgcn_csr_side_classes) */
+    int32_t part_rows[2];  /* the part_rows0 / part_rows1 the classes were built from */
+} lgcn_sides_t;
 int lgcn_propagate_forward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
-                                 const int32_t* row_ids, int32_t n, int32_t split,
+                                 const int32_t* row_ids, const lgcn_sides_t* sides,
                                  const lgcn_hub_plan_t* plans, lgcn_rows_t emb, int32_t d,
                                  int32_t K, float* const* layer_bufs_host, float* out,
                                  const lgcn_sched_t* sched, void* stream);
 int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edges,
-                                  const int32_t* row_ids, int32_t n, int32_t split,
+                                  const int32_t* row_ids, const lgcn_sides_t* sides,
                                   const lgcn_hub_plan_t* plans, lgcn_rows_t grad_out,
                                   const uint32_t* grad_nz, int32_t d, int32_t K, float* work_h,
                                   float* grad_e0, const lgcn_sched_t* sched, void* stream);

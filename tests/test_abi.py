@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 12
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 13
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 
@@ -109,15 +109,6 @@ def test_argument_validation_without_gpu(lib):
                                None) == -1    # unsupported width
     # (+ padding, emu_live, emu_part_max_blocks)
     assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8 + 8
-    # chunk windows: a window must be non-empty; row windows of at most 65535 rows
-    assert lib.lgcn_emu_walk_chunks(None, None, None, 2, None, None, None, rows, 1.0, None, None,
-                                    64, 64, ctypes.byref(ep), 8, None, 4, 4, None) == -1
-    assert lib.lgcn_emu_walk_chunks(None, None, None, 2, None, None, None, rows, 1.0, None, None,
-                                    64, 64, ctypes.byref(ep), 8, None, -1, 4, None) == -1
-    assert lib.lgcn_emu_blocks_rows(None, None, None, 70000, 0, 4, rows, 1.0, None, 64, None,
-                                    None, None, None, None) == -1
-    assert lib.lgcn_emu_blocks_rows(None, None, None, 2, 4, 4, rows, 1.0, None, 64, None, None,
-                                    None, None, None) == 0   # empty window: nothing to do
     # live-edge rows: the row mask and the scratch are required, widths as the chain kernel's
     assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, None, None, 64, 64,
                               ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # no x_nz
@@ -146,11 +137,21 @@ def test_argument_validation_without_gpu(lib):
     assert lib.lgcn_csr_check_bipartite(None, None, None, 10, 5, 3, 2, None, None) == -1
     assert lib.lgcn_csr_check_bipartite(None, None, None, 10, 0, 2, 3, ctypes.c_void_p(4),
                                         None) == 0   # no edges: nothing to check
-    # the sided entry points: four plans and the slot order are required
-    assert lib.lgcn_propagate_forward_sides(None, None, None, 5, 2, None, rows, 64, 2,
+    # the sided entry points: the slot layout, eight plans and the slot order are required
+    sd = engine.SidesT()
+    sd.n, sd.split = 5, 2
+    sd.class_end[0], sd.class_end[1] = 2, 2
+    assert lib.lgcn_propagate_forward_sides(None, None, None, None, None, rows, 64, 2,
                                             None, ctypes.c_void_p(8), None, None) == -1
-    assert lib.lgcn_propagate_backward_sides(None, None, None, 5, 2, None, rows, None, 64, 1,
-                                             None, ctypes.c_void_p(8), None, None) == -1
+    assert lib.lgcn_propagate_forward_sides(None, None, None, ctypes.byref(sd), None, rows, 64, 2,
+                                            None, ctypes.c_void_p(8), None, None) == -1
+    assert lib.lgcn_propagate_backward_sides(None, None, None, ctypes.byref(sd), None, rows, None,
+                                             64, 1, None, ctypes.c_void_p(8), None, None) == -1
+    # side classes: ranges checked before anything runs
+    for split, p0, p1 in ((11, 0, 0), (4, 3, 2), (4, 0, 7)):
+        assert lib.lgcn_csr_side_classes(None, None, None, 10, 0, split, p0, p1, None, None, None,
+                                         None, None, None, ctypes.byref(nbytes), None) == -1
+    assert lib.lgcn_sched_state(None, engine.SCHED_STATE_LANES) == -1
 
 
 def test_struct_layout_matches_header():
@@ -195,7 +196,7 @@ def test_tune_knobs(lib):
     """lgcn_tune: every knob answers its previous value (a negative value only queries), an
     unknown knob is refused; knobs never change results (tested on the GPU)."""
     for knob in (engine.TUNE_ROWS_PER_GROUP, engine.TUNE_UNROLL, engine.TUNE_MEAN_PREFETCH,
-                 engine.TUNE_MIN_GROUPS, engine.TUNE_EMU_RESOLVE):
+                 engine.TUNE_MIN_GROUPS, engine.TUNE_EMU_MARGIN):
         old = lib.lgcn_tune(knob, -1)
         assert old >= 0
         assert lib.lgcn_tune(knob, 7) == old

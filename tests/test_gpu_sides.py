@@ -7,7 +7,9 @@ Bar: BITWISE against the oracle's sequential fmaf chain (models/lightgcn.py:45's
 on CPU), forward and backward, with hub rows on both sides (brand rows are the side-0 hubs), for
 every stream budget: two lanes with their own aux streams (7), a lane without aux streams (4),
 both lanes on one stream set (3), no schedule at all; and through autograd (propagate_blocks) and
-a captured HIP graph."""
+a captured HIP graph. The side-0 classes (lgcn_csr_side_classes: users linked to the walked
+item rows of part 0 / part 1 / neither) and the dependency schedule built on them are checked
+with all three classes populated, and with classes off (graph and schedule)."""
 import numpy as np
 import pytest
 import torch
@@ -48,31 +50,73 @@ def _segs(x, dev):
 KW = dict(hub_threshold=128, hub_mode="exact", emu_min=256)
 
 
+def _classes_env(monkeypatch, classes):
+    """Walk cuts small enough for the brand graph to have all three side-0 classes: part 0 =
+    item rows of more than 40 blocks (~10k edges), part 1 = more than 8 (2048-edge chain cut)."""
+    monkeypatch.setenv("LGCN_EMU_PART0", "40")
+    monkeypatch.setenv("LGCN_CHAIN_MAX", "2048")
+    monkeypatch.setenv("LGCN_CLASSES", "0" if classes == "graph_off" else "1")
+    if classes == "graph_off":
+        monkeypatch.setenv("LGCN_CLASSES", "0")
+    if classes == "sched_off":
+        monkeypatch.setenv("LGCN_SCHED_CLASSES", "0")
+
+
+def _check_classes(g, r, c, n):
+    """The class-major slot order: side 0 = users + brands in classes 0 / 1 / 2 by the walked
+    item rows they link to, each class degree-descending; side 1 untouched."""
+    ids = g.row_ids.cpu().numpy()
+    rp = g.rowptr_host().astype(np.int64)
+    deg = np.diff(rp)
+    c0, c1 = g.class_end
+    p0, p01 = g.class_parts
+    assert 0 < c0 < c1 < g.split and 0 < p0 < p01   # every class populated
+    part = {int(x): (0 if k < p0 else 1) for k, x in enumerate(ids[g.split:g.split + p01])}
+    for cls, (a, b) in enumerate(((0, c0), (c0, c1), (c1, g.split))):
+        assert (np.diff(deg[a:b]) <= 0).all()
+        for s_ in range(a, b, max(1, (b - a) // 200)):   # a sample of each class
+            row = ids[s_]
+            nb = c[np.searchsorted(r, row):np.searchsorted(r, row + 1)]
+            got = min([part[int(x)] for x in nb if int(x) in part], default=2)
+            assert got == cls, (s_, row, got, cls)
+
+
 @pytest.mark.parametrize("n_aux", [7, 4, 3, 0])
 @pytest.mark.parametrize("kind", ["xavier", "few_bits"])
-def test_sides_bitwise(gpu_device, monkeypatch, brand_graph, n_aux, kind):
+@pytest.mark.parametrize("classes", ["on", "graph_off", "sched_off"])
+def test_sides_bitwise(gpu_device, monkeypatch, brand_graph, n_aux, kind, classes):
     monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
     if n_aux == 0:
         monkeypatch.setenv("LGCN_EMU_OVERLAP", "0")
     else:
         monkeypatch.setenv("LGCN_AUX_STREAMS", str(n_aux))
+    _classes_env(monkeypatch, classes)
     r, c, v, n = brand_graph
     g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
     assert g.split == n - I and g.sides == (U, U + I)
     ids = g.row_ids.cpu().numpy()
     assert ((ids[g.split:] >= U) & (ids[g.split:] < U + I)).all()
+    assert ((ids[:g.split] < U) | (ids[:g.split] >= U + I)).all()
+    assert np.array_equal(np.sort(ids), np.arange(n))
+    if classes == "graph_off":
+        assert g.class_end in (None, (g.split, g.split))
+    else:
+        _check_classes(g, r, c, n)
     hps = g.side_hubs(128, mode="exact", emu_min=256)
-    assert hps[1].n_emu_rows >= 5 and hps[0].n_emu_rows >= 1   # item and brand hubs
+    assert hps[3].n_emu_rows >= 5 and sum(h.n_emu_rows for h in hps[:3]) >= 1  # item, brand hubs
     rng = np.random.default_rng(5)
     e0 = _e0(rng, kind, n, 64)
     x = _segs(e0, gpu_device)
-    for K in (1, 2, 3):
+    for K in (1, 2, 3, 4):
         want = oracle.forward(r, c, v, e0, K)
         got = engine.propagate_forward(g, x, K, **KW).cpu().numpy()
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (kind, K)
+        if n_aux:  # the library reports what it ran
+            assert engine.last_schedule["lanes"] == (2 if n_aux >= 4 else 1)
+            assert engine.last_schedule["classes"] == (classes == "on" and n_aux > 0)
     G = _e0(rng, "xavier", n, 64)
     G[rng.random(n) > 0.05] = 0.0   # a BPR batch's row-sparse gradient
-    for K in (1, 3):
+    for K in (1, 3, 4):
         want_b = oracle.backward(r, c, v, G, K)
         for sparse in ("off", "on"):
             got_b = engine.propagate_backward(g, _segs(G, gpu_device), K, sparse=sparse,
@@ -103,8 +147,10 @@ def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):
     assert np.array_equal(got_b, oracle.backward(r, c, v, G, 3))
     x = [t.detach() for t in w]
     cap = engine.CapturedForward(g, x, 3, hub_threshold=128)
-    # the capture ran the two lanes (lane 1 without its own aux streams: make_lanes' rule)
-    assert engine.last_schedule == {"sided": True, "aux_streams": 7, "lanes": 2, "captured": True}
+    # the capture ran the two lanes (lane 1 without its own aux streams: the library's default
+    # under a capture, LGCN_SCHED_CAPTURE_AUX)
+    s = engine.last_schedule
+    assert (s["lanes"], s["lane1_aux"], s["captured"], s["aux_streams"]) == (2, 0, True, 7)
     for _ in range(2):
         assert np.array_equal(cap.replay().cpu().numpy(), want)
 
@@ -169,14 +215,40 @@ def test_default_environment_runs_two_lanes(gpu_device, monkeypatch, brand_graph
     import os
     monkeypatch.delenv("LGCN_AUX_STREAMS", raising=False)
     monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
-    assert os.environ.get("GPU_MAX_HW_QUEUES") in (None, "", "4"), "not the default environment"
+    if os.environ.get("GPU_MAX_HW_QUEUES") not in (None, "", "4"):
+        pytest.skip("GPU_MAX_HW_QUEUES is set: not the default environment")
     assert engine.n_aux_streams() == 7
     r, c, v, n = brand_graph
     adj = _adj(r, c, v, n, gpu_device)
     e0 = _e0(np.random.default_rng(12), "xavier", n, 64)
     w = _segs(e0, gpu_device)
     out = engine.propagate_blocks(adj, w, 3, hub_threshold=128)
-    assert engine.last_schedule == {"sided": True, "aux_streams": 7, "lanes": 2,
-                                    "captured": False}
+    s = engine.last_schedule
+    assert (s["lanes"], s["lane1_aux"], s["captured"], s["aux_streams"]) == (2, 3, False, 7)
     got = torch.cat([o.detach() for o in out]).cpu().numpy()
     assert np.array_equal(got, oracle.forward(r, c, v, e0, 3))
+
+
+@pytest.mark.parametrize("K", [3, 4])
+def test_capture_with_lane1_aux_streams(gpu_device, monkeypatch, brand_graph, K):
+    """LGCN_SCHED_CAPTURE_AUX = 1: the captured forward forks lane 1's own aux streams too (every
+    event record of a call on its own event), all three classes populated; replays bitwise,
+    inputs updated in place are seen."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
+    monkeypatch.setenv("LGCN_CAPTURE_AUX", "1")
+    _classes_env(monkeypatch, "on")
+    r, c, v, n = brand_graph
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    rng = np.random.default_rng(17)
+    e0 = _e0(rng, "xavier", n, 64)
+    x = _segs(e0, gpu_device)
+    cap = engine.CapturedForward(g, x, K, hub_threshold=128)
+    s = engine.last_schedule
+    # (under a capture every half-layer joins its parts: no class dependencies, lgcn_engine.hip)
+    assert (s["lanes"], s["lane1_aux"], s["captured"], s["classes"]) == (2, 3, True, False)
+    assert np.array_equal(cap.replay().cpu().numpy(), oracle.forward(r, c, v, e0, K))
+    e1 = _e0(rng, "xavier", n, 64)
+    for t, a in zip(x, _segs(e1, gpu_device)):
+        t.copy_(a)
+    assert np.array_equal(cap.replay().cpu().numpy(), oracle.forward(r, c, v, e1, K))
