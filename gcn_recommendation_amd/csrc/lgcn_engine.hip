@@ -561,6 +561,34 @@ int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int
     return 0;
 }
 
+int32_t lgcn_emu_min_default(int64_t nnz) {
+    // rows up to this degree run as whole-row items of the layer kernel (dispatched first in its
+    // grid); at 2^23+ nonzeros that beats a chain kernel launched beside it (C3: 14.0-14.4 ->
+    // 12.6-13.0 ms, round 4); on a small graph a 1024-edge item is the layer's tail (C2: 0.81 ->
+    // 1.14 ms), so none
+    return nnz >= (int64_t)1 << 23 ? 1024 : 0;
+}
+
+int lgcn_plan_items(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,
+                    int32_t threshold, int32_t emu_min_degree, lgcn_hub_item_t* items_host,
+                    int32_t* n_items_host) {
+    if (!n_items_host || n_rows < 0 || (n_rows > 0 && !rowptr_host) || threshold < 0)
+        return LGCN_EINVAL;
+    int32_t m = 0;
+    for (int32_t s = 0; s < n_rows; ++s) {
+        const int64_t deg = (int64_t)rowptr_host[s + 1] - rowptr_host[s];
+        if (deg < 0) return LGCN_EINVAL;
+        if (deg > threshold && deg <= emu_min_degree) {
+            if (items_host)
+                items_host[m] = lgcn_hub_item_t{row_ids_host ? row_ids_host[s] : s,
+                                                rowptr_host[s], rowptr_host[s + 1], -1};
+            ++m;
+        }
+    }
+    *n_items_host = m;
+    return 0;
+}
+
 int lgcn_plan_scratch_bytes(const lgcn_hub_plan_t* plan, int32_t d, int32_t walk_all,
                             size_t* bytes_host) {
     if (!plan || !bytes_host || d < 1 || d > 2048) return LGCN_EINVAL;

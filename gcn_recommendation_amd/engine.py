@@ -52,12 +52,10 @@ HUB_MODES = ("exact", "chunk")
 # group's chain each (LGCN_EMU_MIN_DEGREE; hub items dispatched first in its grid); longer rows go
 # to the emulated-row list, where the shorter ones run as sequential chains of their own
 # (lgcn_chain_rows, beside the layer kernel) and the longest are block-emulated (emu_parts).
-# Default by graph size: 0 (none) below 2^23 nonzeros, 1024 above — at C3 the
-# rows of 129..1024 edges (most of the ~12k chain rows) were a chain kernel whose grid waited
+# Default by graph size (lgcn_emu_min_default): 0 (none) below 2^23 nonzeros, 1024 above — at C3
+# the rows of 129..1024 edges (most of the ~12k chain rows) were a chain kernel whose grid waited
 # behind the layer kernel's on a shared dispatch pipe; inside the layer kernel: forward 14.0-14.4
 # -> 12.6-13.0 ms (sweep 512 / 1024 / 1536 / 2048: 12.9-13.0 / 12.6-13.0 / 12.7-13.1 / 12.7-13.3)
-DEFAULT_EMU_MIN_DEGREE = 0
-DEFAULT_EMU_MIN_DEGREE_LARGE = 1024
 
 
 def hub_mode_from_env():
@@ -74,12 +72,12 @@ def emu_stage_enabled():
 
 
 def emu_min_degree_from_env(nnz=None):
-    """LGCN_EMU_MIN_DEGREE, else the default for a graph of nnz nonzeros (None: small)."""
+    """LGCN_EMU_MIN_DEGREE, else the library's default for a graph of nnz nonzeros
+    (lgcn_emu_min_default; None: small)."""
     v = os.environ.get("LGCN_EMU_MIN_DEGREE", "")
     if v:
         return int(v)
-    return DEFAULT_EMU_MIN_DEGREE_LARGE if nnz is not None and nnz >= (1 << 23) \
-        else DEFAULT_EMU_MIN_DEGREE
+    return int(load_library().lgcn_emu_min_default(int(nnz or 0)))
 
 
 def chain_max_degree(nnz):
@@ -175,6 +173,8 @@ ABI = [
                                             ctypes.c_float, _P, _I64, _P]),
     ("lgcn_chain_max_default", ctypes.c_int32, [_I64]),
     ("lgcn_plan_exact", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
+    ("lgcn_emu_min_default", ctypes.c_int32, [_I64]),
+    ("lgcn_plan_items", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     ("lgcn_plan_scratch_bytes", ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(ctypes.c_size_t)]),
     ("lgcn_eval_splits", ctypes.c_int, [_I32, _I32, _I32]),
     ("lgcn_score_topk", ctypes.c_int, [_P, _I64, _P, _I32, _P, _I64, _I32, _I32, _P, _P, _I32,
@@ -500,6 +500,25 @@ def plan_emulation(rowptr_host, min_degree, device, row_ids_host=None):
             rows[:, 2].astype(np.int64))
 
 
+def plan_items(rowptr_host, threshold, emu_min, row_ids_host=None):
+    """Whole-row items (int32 [n, 4], lgcn_hub_item_t) of the rows of threshold < degree <=
+    emu_min: the C planner lgcn_plan_items."""
+    lib = load_library()
+    rp = np.ascontiguousarray(rowptr_host, dtype=np.int32)
+    n = rp.size - 1
+    ids = None if row_ids_host is None else np.ascontiguousarray(row_ids_host, dtype=np.int32)
+    ids_p = None if ids is None else ids.ctypes.data
+    m = ctypes.c_int32(0)
+    _check(lib.lgcn_plan_items(rp.ctypes.data, ids_p, n, int(min(threshold, INT32_MAX)),
+                               int(emu_min), None, ctypes.byref(m)), "lgcn_plan_items(size)")
+    items = np.empty((m.value, 4), np.int32)
+    if m.value:
+        _check(lib.lgcn_plan_items(rp.ctypes.data, ids_p, n, int(min(threshold, INT32_MAX)),
+                                   int(emu_min), items.ctypes.data, ctypes.byref(m)),
+               "lgcn_plan_items")
+    return items
+
+
 def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_group=None,
               mode="exact", emu_min=None):
     """Plan the rows with degree > threshold (host planner, numpy). rowptr_host is in storage
@@ -521,9 +540,7 @@ def plan_hubs(rowptr_host, threshold, chunk, device, row_ids_host=None, pre_grou
         return HubPlan(threshold, mode, chunk, emu_min=emu_min)
     out_row = hub if row_ids_host is None else row_ids_host[hub]
     if mode == "exact":
-        long_ = deg[hub] <= emu_min
-        items = np.stack([out_row[long_], rowptr_host[hub[long_]], rowptr_host[hub[long_] + 1],
-                          np.full(int(long_.sum()), -1)], 1).astype(np.int32)
+        items = plan_items(rowptr_host, threshold, emu_min, row_ids_host)
         eb, er, enb = plan_emulation(rowptr_host, max(threshold, emu_min), device,
                                      row_ids_host)
         return HubPlan(threshold, mode, None,

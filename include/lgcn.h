@@ -187,6 +187,18 @@ int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int
                     int32_t emu_min_degree, int32_t chain_max, int32_t part0_blocks,
                     lgcn_emu_row_t* rows_host, lgcn_emu_block_t* blocks_host,
                     lgcn_hub_plan_t* plan);
+/* Whole-row items of an exact plan (host memory only): every row (slot) of threshold < degree <=
+ * emu_min_degree becomes one lgcn_hub_item_t {row, beg, end, slot = -1}, in slot order — the
+ * layer kernel runs each as one sequential chain with the epilogue in place, dispatched first in
+ * its grid; lgcn_plan_exact(..., emu_min_degree, ...) then emulates / chains only the longer
+ * rows. Two-call protocol: items_host = NULL writes only *n_items_host. Copy the items to the
+ * device for plan->items / n_items. lgcn_emu_min_default(nnz) is the engine's default
+ * emu_min_degree for a graph of nnz nonzeros (1024 from 2^23 nonzeros, else 0 = no items): the
+ * headline C3 plan, as engine.plan_hubs builds it. */
+int32_t lgcn_emu_min_default(int64_t nnz);
+int lgcn_plan_items(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,
+                    int32_t threshold, int32_t emu_min_degree, lgcn_hub_item_t* items_host,
+                    int32_t* n_items_host);
 /* Scratch of a plan at width d: bytes_host[0..2] = emu_rel, emu_meta, emu_stage sizes covering
  * the walked blocks (walk_all = 0: parts 0 and 1; 1: every emulated block, when chains cannot
  * run — lgcn_chain_supported(d) false or X not 16-B aligned). */

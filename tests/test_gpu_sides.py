@@ -252,3 +252,59 @@ def test_capture_with_lane1_aux_streams(gpu_device, monkeypatch, brand_graph, K)
     for t, a in zip(x, _segs(e1, gpu_device)):
         t.copy_(a)
     assert np.array_equal(cap.replay().cpu().numpy(), oracle.forward(r, c, v, e1, K))
+
+
+@pytest.mark.parametrize("classes", ["on", "graph_off"])
+def test_c_host_plans_sided_bitwise(gpu_device, monkeypatch, brand_graph, classes):
+    """What a C host runs: plans from the C planner alone (lgcn_plan_items for
+    the whole-row items, lgcn_plan_exact for the emulated / chain rows, lgcn_plan_scratch_bytes;
+    tools/c_host_plans.py), the slot layout in lgcn_sides_t, one lgcn_propagate_forward_sides /
+    _backward_sides call each — bitwise against the oracle and the Python binding."""
+    import ctypes
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    from c_host_plans import c_host_side_plans
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
+    _classes_env(monkeypatch, classes)
+    r, c, v, n = brand_graph
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    lib = engine.load_library()
+    d, K = 64, 3
+    chain_max = int(engine.chain_max_degree(g.nnz))   # (LGCN_CHAIN_MAX of _classes_env)
+    plans, keep = c_host_side_plans(lib, g.rowptr_host(), g.row_ids_host(), g.segments(), g.nnz,
+                                    d, gpu_device, emu_min=256, chain_max=chain_max)
+    assert sum(plans[2 * s].n_items for s in range(4)) > 0       # whole-row items present
+    assert plans[6].emu_part_rows[1] > 0                          # walked item rows
+    rng = np.random.default_rng(23)
+    e0 = _e0(rng, "xavier", n, d)
+    x = _segs(e0, gpu_device)
+    sides = g.sides_struct()
+    sc = engine.sched_for(gpu_device)
+    layers = [torch.empty((n, d), device=gpu_device) for _ in range(K - 1)]
+    out = torch.empty((n, d), device=gpu_device)
+    bufs = (ctypes.c_void_p * (K - 1))(*[t.data_ptr() for t in layers])
+    P = engine._ptr
+    st = engine._stream(gpu_device)
+    rc = lib.lgcn_propagate_forward_sides(P(g.rowptr), P(g.edges), P(g.row_ids),
+                                          ctypes.byref(sides), plans, engine.rows_desc(x, d), d, K,
+                                          bufs, P(out), sc.handle, st)
+    assert rc == 0
+    want = oracle.forward(r, c, v, e0, K)
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert torch.equal(out, engine.propagate_forward(g, x, K, hub_threshold=128, hub_mode="exact",
+                                                     emu_min=256))
+    gt = g.transpose
+    G = _e0(rng, "xavier", n, d)
+    plans_t, keep_t = c_host_side_plans(lib, gt.rowptr_host(), gt.row_ids_host(), gt.segments(),
+                                        gt.nnz, d, gpu_device, emu_min=256, chain_max=chain_max)
+    work = torch.empty((n, d), device=gpu_device)
+    ge0 = torch.empty((n, d), device=gpu_device)
+    sides_t = gt.sides_struct()
+    rc = lib.lgcn_propagate_backward_sides(P(gt.rowptr), P(gt.edges), P(gt.row_ids),
+                                           ctypes.byref(sides_t), plans_t,
+                                           engine.rows_desc(_segs(G, gpu_device), d), None, d, K,
+                                           P(work), P(ge0), sc.handle, st)
+    assert rc == 0
+    assert np.array_equal(ge0.cpu().numpy(), oracle.backward(r, c, v, G, K))

@@ -1,7 +1,8 @@
 """The C host path vs the Python path at C3: the forward as a C host drives it (one
-lgcn_propagate_forward_sides call with the plans from lgcn_plan_exact and a 7-stream
-lgcn_sched_t) against engine.propagate_forward, same graph, median of
-REPS; and their outputs compared bitwise.
+lgcn_propagate_forward_sides call with plans built by the C planner alone — lgcn_plan_items +
+lgcn_plan_exact per segment, tools/c_host_plans.py — and a 7-stream lgcn_sched_t,
+INTEGRATION.md §2) against engine.propagate_forward, same graph, median of REPS; and their
+outputs compared bitwise.
 
     python tools/c_abi_timing.py
 """
@@ -14,7 +15,9 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 import bench  # noqa: E402
+from c_host_plans import c_host_side_plans  # noqa: E402
 from gcn_recommendation_amd import engine  # noqa: E402
 
 
@@ -46,10 +49,11 @@ def main():
     assert g.split is not None
     gen = torch.Generator().manual_seed(42)
     segs = [bench.xavier(U, d, gen).to(dev), bench.xavier(I, d, gen).to(dev)]
-    # the C host's objects: 4 plans (2 sides x 2 scratch sets), the schedule, the buffers
-    # (the plans the engine builds: at C3 scale rows of 129..1024 edges are whole-row items of
-    # the layer kernel, emu_min = engine.emu_min_degree_from_env(nnz))
-    plans, _ = engine._side_plans(g, d, 128, "exact", engine.emu_min_degree_from_env(g.nnz), True)
+    # the C host's objects: 8 plans (4 segments x 2 scratch sets) from the C planner alone, the
+    # schedule, the buffers
+    plans, keep = c_host_side_plans(lib, g.rowptr_host(), g.row_ids_host(), g.segments(), g.nnz,
+                                    d, dev)
+    sides = g.sides_struct()
     sc = engine.sched_for(dev)
     layers = [torch.empty((n, d), device=dev) for _ in range(K - 1)]
     out_c = torch.empty((n, d), device=dev)
@@ -59,15 +63,19 @@ def main():
 
     def c_host():
         rc = lib.lgcn_propagate_forward_sides(
-            P(g.rowptr), P(g.edges), P(g.row_ids), n, g.split, plans, e0, d, K, bufs, P(out_c),
-            sc.handle, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            P(g.rowptr), P(g.edges), P(g.row_ids), ctypes.byref(sides), plans, e0, d, K, bufs,
+            P(out_c), sc.handle, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert rc == 0, lib.lgcn_error_string(rc)
     out_py = [None]
 
     def python():
         out_py[0] = engine.propagate_forward(g, segs, K)
-    t_c = median_ms(c_host, reps)
-    t_py = median_ms(python, reps)
+    # interleaved: box-to-box and run-to-run drift hits both sides alike
+    t_c, t_py = [], []
+    for _ in range(3):
+        t_c.append(median_ms(c_host, reps))
+        t_py.append(median_ms(python, reps))
+    t_c, t_py = float(np.median(t_c)), float(np.median(t_py))
     same = bool(torch.equal(out_c, out_py[0]))
     print(f"C host lgcn_propagate_forward_sides: {t_c:.3f} ms; engine.propagate_forward: "
           f"{t_py:.3f} ms; ratio {t_c / t_py:.3f}; outputs bitwise equal: {same}", flush=True)
