@@ -1102,11 +1102,24 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
             if (int e = herr(hipEventRecord(sc->t1, st))) return e;
         return hub_combine(p.rows, p.n_rows, p.n_pre, p.partials, y, ldy, d, ep, st);
     };
+    // a MEAN whose operands arrive late (the other lane's layer K-1) with an emu_out scratch: the
+    // walks and chains write their rows' sums there (LGCN_EPI_ROWS) without waiting for them, and
+    // the mean of those rows follows on `s` once they are ready (lgcn_emu_epilogue)
+    const bool has_late = dp && (dp->late[0] || dp->late[1] || dp->late[2]);
+    const bool defer_epi = sc && has_late && ep.mode == LGCN_EPI_MEAN && p.emu_out && ne > 0 &&
+                           !live;
+    lgcn_epilogue_t ep_rows;
+    memset(&ep_rows, 0, sizeof(ep_rows));
+    ep_rows.mode = LGCN_EPI_ROWS;
+    // where the emulated rows of part i go: Y, or emu_out rows [r0, r1) when deferred
+    auto emu_y = [&](int i) { return defer_epi ? p.emu_out + (int64_t)parts[i].r0 * d : y; };
+    const int64_t emu_ld = defer_epi ? d : ldy;
+    const lgcn_epilogue_t& emu_ep = defer_epi ? ep_rows : ep;
     auto chain_rows = [&](hipStream_t st) -> int {
         const EmuPart& q = parts[2];
         if (q.r1 <= q.r0) return 0;
-        return lgcn_chain_rows(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, x, xdiv, y,
-                               ldy, d, &ep, st);
+        return lgcn_chain_rows(edges, p.emu_blocks, p.emu_rows + q.r0, q.r1 - q.r0, x, xdiv,
+                               emu_y(2), emu_ld, d, &emu_ep, st);
     };
     // live path: the live-edge chains take every chain row (part 2) and every walked row with at
     // most LGCN_LIVE_MAX live edges; block pass + walk run the rest (their waves of the live
@@ -1196,10 +1209,11 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
                 if (int e = mark(1 + i, aux_of(i))) return e;
         }
     // the block passes read X only; every kernel after them writes Y, whose epilogue operands
-    // are ready once `late` fires
+    // are ready once `late` fires (the walks and chains write emu_out instead when deferred)
     if (int e = wait_late(s, dp)) return e;
-    for (int i = 0; i < na; ++i)
-        if (int e = wait_late(sc->aux[i], dp)) return e;
+    if (!defer_epi)
+        for (int i = 0; i < na; ++i)
+            if (int e = wait_late(sc->aux[i], dp)) return e;
     // the layer kernel waits for part 0's block pass
     if (parts[0].b1 > parts[0].b0)
         if (int e = link(sc, aux_of(0), s)) return e;
@@ -1211,8 +1225,8 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     }
     for (int i = 0; i < 3; ++i)
         if (i < 2 || !chains) {
-            if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, y, ldy, d, ep, slots[i],
-                                  nullptr, aux_of(i)))
+            if (int e = part_walk(edges, p, parts[i], x, xdiv, x_nz, emu_y(i), emu_ld, d, emu_ep,
+                                  slots[i], nullptr, aux_of(i)))
                 return e;
             if (i < 2)
                 if (int e = mark(5 + i, aux_of(i))) return e;
@@ -1225,6 +1239,8 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
             return e;
         }
     }
+    if (defer_epi)
+        if (int e = lgcn_emu_epilogue(p.emu_rows, ne, p.emu_out, d, y, ldy, d, &ep, s)) return e;
     if (int e = mark(7, s)) return e;
     return own ? 0 : done_on_s();
 }

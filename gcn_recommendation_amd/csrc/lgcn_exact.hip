@@ -40,6 +40,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "lgcn.h"
@@ -879,6 +880,10 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     if (lane != 0) return;
     const int32_t row = er.row;
     float out = __uint_as_float(ab);
+    if constexpr (MODE == LGCN_EPI_ROWS) {  // the chain value itself, to row i of the list
+        y[(int64_t)blockIdx.x * ldy + c] = out;
+        return;
+    }
     if constexpr (MODE == LGCN_EPI_MEAN) {
         // ((E0 + E1) + ... + E_{K-1}) + E_K, then / (K+1)  (lightgcn.py:54)
         float s = seg_row_x(ep.prev0, row)[c];
@@ -1126,6 +1131,10 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     const int c = c0 + lane;
     const int32_t row = er.row;
     float out = acc;
+    if constexpr (MODE == LGCN_EPI_ROWS) {  // the chain value itself, to row i of the list
+        y[(int64_t)blockIdx.x * ldy + c] = out;
+        return;
+    }
     if constexpr (MODE == LGCN_EPI_MEAN) {
         float s = seg_row_x(ep.prev0, row)[c];
         for (int i = 0; i + 1 < ep.n_prev; ++i) s = s + ep.prev_dense[i][(int64_t)row * ep.ld_prev + c];
@@ -1179,6 +1188,33 @@ int chain_mode(int xd, const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         default: return LGCN_EINVAL;
     }
 }
+// The epilogue of emulated rows a walk / chain wrote with LGCN_EPI_ROWS (their chain values, row
+// i of the list in tmp row i), applied once the epilogue's operands are ready: the same
+// arithmetic, in the same order, as the kernels' own epilogue.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_emu_epilogue(const lgcn_emu_row_t* __restrict__ rows,
+                                                      const float* __restrict__ tmp, int64_t ldt,
+                                                      float* __restrict__ y, int64_t ldy,
+                                                      int32_t d, lgcn_epilogue_t ep) {
+    const int32_t row = rows[blockIdx.x].row;
+    for (int c = threadIdx.x; c < d; c += blockDim.x) {
+        float out = tmp[(int64_t)blockIdx.x * ldt + c];
+        if constexpr (MODE == LGCN_EPI_MEAN) {
+            float s = seg_row_x(ep.prev0, row)[c];
+            for (int i = 0; i + 1 < ep.n_prev; ++i)
+                s = s + ep.prev_dense[i][(int64_t)row * ep.ld_prev + c];
+            s = s + out;
+            out = ep.pad ? s * __int_as_float(ep.pad) : s / ep.div;
+        } else if constexpr (MODE == LGCN_EPI_ADD) {
+            if (!ep.addend_nz || row_live_x(ep.addend_nz, row)) {
+                const float z = seg_row_x(ep.addend, row)[c];
+                out = (ep.pad ? z * __int_as_float(ep.pad) : z / ep.div) + out;
+            }
+        }
+        y[(int64_t)row * ldy + c] = out;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // row-sparse X (the backward's first layer on a BPR batch's gradient): emulated rows as chains
 // over their LIVE edges only
@@ -1395,9 +1431,10 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     if (ep.mode == LGCN_EPI_MEAN && (ep.n_prev < 1 || ep.n_prev - 1 > LGCN_MAX_LAYERS))
         return LGCN_EINVAL;
     if (ep.mode == LGCN_EPI_ADD && !ep.addend.p0) return LGCN_EINVAL;
-    if (ep.mode != LGCN_EPI_STORE && !(ep.div > 0.f)) return LGCN_EINVAL;
+    if ((ep.mode == LGCN_EPI_MEAN || ep.mode == LGCN_EPI_ADD) && !(ep.div > 0.f)) return LGCN_EINVAL;
+    if (ep.mode < LGCN_EPI_STORE || ep.mode > LGCN_EPI_ROWS) return LGCN_EINVAL;
     // a power-of-two divisor becomes a multiply by its exact reciprocal (same rounding)
-    if (ep.mode != LGCN_EPI_STORE && is_pow2(ep.div)) {
+    if ((ep.mode == LGCN_EPI_MEAN || ep.mode == LGCN_EPI_ADD) && is_pow2(ep.div)) {
         const float inv = 1.0f / ep.div;
         memcpy(&ep.pad, &inv, sizeof(inv));
     } else {
@@ -1415,9 +1452,45 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
             return walk_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
         case LGCN_EPI_ADD:
             return walk_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s);
+        case LGCN_EPI_ROWS:  // (a forward's deferred mean: X read as is)
+            return xd == 0 ? launch_walk<LGCN_EPI_ROWS, 0>(edges, blocks, rows, n_rows, kp, mp, stage, x, xa, x_nz, y, ldy, d, ep, slots, live, s) : LGCN_EINVAL;
         default:
             return LGCN_EINVAL;
     }
+}
+
+int lgcn_emu_epilogue(const lgcn_emu_row_t* rows, int32_t n_rows, const float* tmp, int64_t ld_tmp,
+                      float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                      void* stream) {
+    if (n_rows < 0 || d < 1 || d > 2048 || !epi_host) return LGCN_EINVAL;
+    if (n_rows == 0) return 0;
+    if (!rows || !tmp || !y || ld_tmp < d || ldy < d) return LGCN_EINVAL;
+    lgcn_epilogue_t ep = *epi_host;
+    if (ep.mode < LGCN_EPI_STORE || ep.mode > LGCN_EPI_ADD) return LGCN_EINVAL;
+    if (ep.mode == LGCN_EPI_MEAN && (ep.n_prev < 1 || ep.n_prev - 1 > LGCN_MAX_LAYERS))
+        return LGCN_EINVAL;
+    if (ep.mode == LGCN_EPI_ADD && !ep.addend.p0) return LGCN_EINVAL;
+    if ((ep.mode == LGCN_EPI_MEAN || ep.mode == LGCN_EPI_ADD) && !(ep.div > 0.f)) return LGCN_EINVAL;
+    if ((ep.mode == LGCN_EPI_MEAN || ep.mode == LGCN_EPI_ADD) && is_pow2(ep.div)) {
+        const float inv = 1.0f / ep.div;
+        memcpy(&ep.pad, &inv, sizeof(inv));
+    } else {
+        ep.pad = 0;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((uint32_t)n_rows), block((uint32_t)std::min(d, 256));
+    switch (ep.mode) {
+        case LGCN_EPI_STORE:
+            hipLaunchKernelGGL(k_emu_epilogue<LGCN_EPI_STORE>, grid, block, 0, s, rows, tmp, ld_tmp, y, ldy, d, ep);
+            break;
+        case LGCN_EPI_MEAN:
+            hipLaunchKernelGGL(k_emu_epilogue<LGCN_EPI_MEAN>, grid, block, 0, s, rows, tmp, ld_tmp, y, ldy, d, ep);
+            break;
+        default:
+            hipLaunchKernelGGL(k_emu_epilogue<LGCN_EPI_ADD>, grid, block, 0, s, rows, tmp, ld_tmp, y, ldy, d, ep);
+            break;
+    }
+    return herr_x(hipGetLastError());
 }
 
 int lgcn_chain_supported(int32_t d) { return d > 0 && d <= 2048 && d % 8 == 0; }
@@ -1438,8 +1511,9 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     if (ep.mode == LGCN_EPI_MEAN && (ep.n_prev < 1 || ep.n_prev - 1 > LGCN_MAX_LAYERS))
         return LGCN_EINVAL;
     if (ep.mode == LGCN_EPI_ADD && !ep.addend.p0) return LGCN_EINVAL;
-    if (ep.mode != LGCN_EPI_STORE && !(ep.div > 0.f)) return LGCN_EINVAL;
-    if (ep.mode != LGCN_EPI_STORE && is_pow2(ep.div)) {
+    if ((ep.mode == LGCN_EPI_MEAN || ep.mode == LGCN_EPI_ADD) && !(ep.div > 0.f)) return LGCN_EINVAL;
+    if (ep.mode < LGCN_EPI_STORE || ep.mode > LGCN_EPI_ROWS) return LGCN_EINVAL;
+    if ((ep.mode == LGCN_EPI_MEAN || ep.mode == LGCN_EPI_ADD) && is_pow2(ep.div)) {
         const float inv = 1.0f / ep.div;
         memcpy(&ep.pad, &inv, sizeof(inv));
     } else {
@@ -1452,6 +1526,8 @@ int lgcn_chain_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
         case LGCN_EPI_STORE: return chain_mode<LGCN_EPI_STORE>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
         case LGCN_EPI_MEAN: return chain_mode<LGCN_EPI_MEAN>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
         case LGCN_EPI_ADD: return chain_mode<LGCN_EPI_ADD>(xd, edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s);
+        case LGCN_EPI_ROWS:
+            return xd == 0 ? launch_chain<LGCN_EPI_ROWS, 0>(edges, blocks, rows, n_rows, x, xa, y, ldy, d, ep, s) : LGCN_EINVAL;
         default: return LGCN_EINVAL;
     }
 }

@@ -65,6 +65,14 @@ def hub_mode_from_env():
     return m
 
 
+def emu_defer_enabled():
+    """A final mean half-layer's walks and chains write their rows' sums to scratch and the mean
+    of those rows follows once the other lane's layer K-1 is done (lgcn_hub_plan_t emu_out), so
+    they start as soon as their block passes are done; LGCN_EMU_DEFER=0 makes them wait (same
+    bits)."""
+    return os.environ.get("LGCN_EMU_DEFER", "1") != "0"
+
+
 def emu_stage_enabled():
     """LGCN_EMU_STAGE=0 turns off the staged X elements of emulated blocks (re-run blocks then
     gather X: one 4-B element per row, a whole memory line each)."""
@@ -128,7 +136,7 @@ class PlanT(ctypes.Structure):
                 ("n_emu_blocks", ctypes.c_int32), ("n_emu_rows", ctypes.c_int32),
                 ("emu_part_rows", ctypes.c_int32 * 2), ("emu_part_blocks", ctypes.c_int32 * 2),
                 ("emu_scratch_blocks", ctypes.c_int32), ("emu_live", ctypes.c_void_p),
-                ("emu_part_max_blocks", ctypes.c_int32 * 2)]
+                ("emu_part_max_blocks", ctypes.c_int32 * 2), ("emu_out", ctypes.c_void_p)]
 
 
 class SidesT(ctypes.Structure):
@@ -190,6 +198,8 @@ ABI = [
     ("lgcn_emu_walk", ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, RowsT, ctypes.c_float, _P, _P,
                                      _I64, _I32, ctypes.POINTER(EpilogueT), _I32, _P, _P]),
     ("lgcn_chain_supported", ctypes.c_int, [_I32]),
+    ("lgcn_emu_epilogue", ctypes.c_int, [_P, _I32, _P, _I64, _P, _I64, _I32,
+                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_live_scratch_bytes", ctypes.c_size_t, [_I32, _I32]),
     ("lgcn_live_rows", ctypes.c_int, [_P, _P, _I32, _P, _I32, RowsT, ctypes.c_float, _P, _P, _I64,
                                       _I32, ctypes.POINTER(EpilogueT), _I32, _I32, _P, _P]),
@@ -402,14 +412,14 @@ class HubPlan:
         return [r0, r1], [int(cum[r0]), int(cum[r1])]
 
     def scratch(self, d, device, n_blocks=None, scratch_set=0):
-        """(partials, emu_rel, emu_meta, emu_stage) for width d, covering the first n_blocks
+        """(partials, emu_rel, emu_meta, emu_stage, emu_out) for width d, covering the first n_blocks
         emulated blocks (the walked ones; default all), allocated once per width and set and
         grown on demand (the layers of one operator run in stream order; the bipartite lanes run
         a side's consecutive layers concurrently, on sets 0 and 1). release_scratch() drops it."""
         n_blocks = self.n_emu_blocks if n_blocks is None else n_blocks
         key = (d, scratch_set)
         have = self._scratch.get(key)
-        if have is None or have[4] < n_blocks:
+        if have is None or have[5] < n_blocks:
             f32 = dict(dtype=torch.float32, device=device)
             part = have[0] if have is not None else (
                 torch.empty(self.n_slots * d, **f32) if self.n_slots else None)
@@ -420,8 +430,11 @@ class HubPlan:
                                    device=device)
                 if emu_stage_enabled():
                     stage = torch.empty(n_blocks * (d + 1) * LGCN_EMU_BLOCK, **f32)
-            self._scratch[key] = (part, rel, meta, stage, n_blocks)
-        return self._scratch[key][:4]
+            # the emulated rows' sums of a deferred mean epilogue (LGCN_EPI_ROWS)
+            out = torch.empty(self.n_emu_rows * d, **f32) if self.n_emu_rows and \
+                emu_defer_enabled() else None
+            self._scratch[key] = (part, rel, meta, stage, out, n_blocks)
+        return self._scratch[key][:5]
 
     def live_scratch(self, device):
         """Scratch of lgcn_live_rows (row-sparse X: the emulated rows as chains over their live
@@ -452,7 +465,7 @@ class HubPlan:
         if nnz is not None:
             rows, blocks = self.walk_parts(nnz)
         need = self.n_emu_blocks if (walk_all or nnz is None) else blocks[1]
-        part, rel, meta, stage = self.scratch(d, device, need, scratch_set)
+        part, rel, meta, stage, eout = self.scratch(d, device, need, scratch_set)
         p = PlanT()
         p.items, p.n_items = (self.items.data_ptr() if self.n_items else None), self.n_items
         p.rows, p.n_rows, p.n_pre = (self.rows.data_ptr() if self.n_entries else None), \
@@ -464,6 +477,7 @@ class HubPlan:
         p.emu_rel = rel.data_ptr() if rel is not None else None
         p.emu_meta = meta.data_ptr() if meta is not None else None
         p.emu_stage = stage.data_ptr() if stage is not None else None
+        p.emu_out = eout.data_ptr() if eout is not None else None
         p.threshold = min(self.threshold, INT32_MAX)
         p.emu_part_rows[0], p.emu_part_rows[1] = rows
         p.emu_part_blocks[0], p.emu_part_blocks[1] = blocks
@@ -984,7 +998,8 @@ def _stream_priorities(n_aux):
     critical path (lgcn_propagate_*_sides); LGCN_LANE_PRIORITY=part0 instead raises each lane's
     part-0 stream (aux 0 and 4), =parts both lanes' walked parts (aux 0, 1, 4, 5: the latency-bound
     block passes and walks), leaving the layer kernels and chains of both lanes at normal
-    priority (4 + 4 streams: one hardware queue each under HIP's default)."""
+    priority, =hub lane 1 but its chains, plus lane 0's part 0 (aux 0, 3, 4, 5) (4 + 4 streams:
+    one hardware queue each under HIP's default)."""
     if n_aux <= 3:
         return [i == 0 for i in range(n_aux)]
     mode = os.environ.get("LGCN_LANE_PRIORITY", "lane1")
@@ -992,6 +1007,8 @@ def _stream_priorities(n_aux):
         return [i in (0, 4) for i in range(n_aux)]
     if mode == "parts":
         return [i in (0, 1, 4, 5) for i in range(n_aux)]
+    if mode == "hub":   # lane 1's main + walked parts, and lane 0's part 0 (its longest walk)
+        return [i in (0, 3, 4, 5) for i in range(n_aux)]
     return [i >= 3 for i in range(n_aux)]
 
 

@@ -61,6 +61,9 @@ extern "C" {
 #define LGCN_EPI_STORE 0  /* Y = Â·X */
 #define LGCN_EPI_MEAN  1  /* Y = (((P0 + P1) + ... + P_{n-1}) + Â·X) / div   (lightgcn.py:54) */
 #define LGCN_EPI_ADD   2  /* Y = Z / div + Â·X          (backward Horner step) */
+#define LGCN_EPI_ROWS  3  /* emulated-row entry points only (lgcn_emu_walk, lgcn_chain_rows): the
+                             sum of row i of the row list to Y row i — an epilogue deferred to
+                             lgcn_emu_epilogue, so a walk need not wait for the epilogue's operands */
 
 typedef int64_t lgcn_edge_t;
 
@@ -168,6 +171,11 @@ typedef struct {
     /* the longest row's block count in part 0 / part 1 (lgcn_plan_exact writes them;
      * informational) */
     int32_t emu_part_max_blocks[2];
+    /* optional (NULL = off) scratch [n_emu_rows x d] fp32, 16-B aligned: a MEAN layer under a
+     * schedule with a late epilogue operand (lgcn_propagate_forward_sides' final half-layers)
+     * writes the emulated rows' sums here (LGCN_EPI_ROWS) and applies their mean once the
+     * operands are ready (lgcn_emu_epilogue), so its walks and chains need not wait for them */
+    float* emu_out;
 } lgcn_hub_plan_t;
 
 /* Host planner of an exact hub plan (host memory only, no GPU call): from the host row pointers
@@ -407,6 +415,13 @@ int lgcn_emu_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                   const float* stage, lgcn_rows_t x, float x_div, const uint32_t* x_nz, float* y,
                   int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, int32_t slots,
                   const lgcn_emu_row_t* live, void* stream);
+
+/* The deferred epilogue of emulated rows written with LGCN_EPI_ROWS: row i of `rows` (output row
+ * rows[i].row) = epilogue(tmp row i) with the STORE / MEAN / ADD epilogue epi_host — the
+ * arithmetic, and order, of the kernels' own epilogue (bitwise the same rows). */
+int lgcn_emu_epilogue(const lgcn_emu_row_t* rows, int32_t n_rows, const float* tmp, int64_t ld_tmp,
+                      float* y, int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host,
+                      void* stream);
 
 /* Mid-size emulated rows run as the reference's sequential chain itself (no block pass): one
  * wave per (row, column slice) folds acc = fma(val_j, X[col_j, c], acc) in stored order from +0

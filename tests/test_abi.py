@@ -107,8 +107,8 @@ def test_argument_validation_without_gpu(lib):
                                None) == 0     # nothing to do
     assert lib.lgcn_chain_rows(None, None, None, 2, rows, 1.0, None, 64, 12, ctypes.byref(ep),
                                None) == -1    # unsupported width
-    # (+ padding, emu_live, emu_part_max_blocks)
-    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8 + 8
+    # (+ padding, emu_live, emu_part_max_blocks, emu_out)
+    assert ctypes.sizeof(engine.PlanT) == 8 * 8 + 6 * 4 + 5 * 4 + 4 + 8 + 8 + 8
     # live-edge rows: the row mask and the scratch are required, widths as the chain kernel's
     assert lib.lgcn_live_rows(None, None, 4, None, 2, rows, 1.0, None, None, 64, 64,
                               ctypes.byref(ep), 0, 0, ctypes.c_void_p(256), None) == -1   # no x_nz

@@ -308,3 +308,22 @@ def test_c_host_plans_sided_bitwise(gpu_device, monkeypatch, brand_graph, classe
                                            P(work), P(ge0), sc.handle, st)
     assert rc == 0
     assert np.array_equal(ge0.cpu().numpy(), oracle.backward(r, c, v, G, K))
+
+
+@pytest.mark.parametrize("defer", ["0", "1"])
+@pytest.mark.parametrize("classes", ["on", "graph_off"])
+def test_mean_epilogue_deferred(gpu_device, monkeypatch, brand_graph, defer, classes):
+    """The final mean half-layers' walks and chains write their rows' sums to emu_out and the
+    mean of those rows follows once the other lane's layer K-1 is done (LGCN_EMU_DEFER=1, the
+    default), or they wait for it (0): bitwise either way, K = 2..4."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
+    monkeypatch.setenv("LGCN_EMU_DEFER", defer)
+    _classes_env(monkeypatch, classes)
+    r, c, v, n = brand_graph
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    e0 = _e0(np.random.default_rng(29), "drift", n, 64)
+    x = _segs(e0, gpu_device)
+    for K in (2, 3, 4):
+        got = engine.propagate_forward(g, x, K, **KW).cpu().numpy()
+        assert np.array_equal(got, oracle.forward(r, c, v, e0, K)), K

@@ -55,15 +55,19 @@ def main():
                                     d, dev)
     sides = g.sides_struct()
     sc = engine.sched_for(dev)
-    layers = [torch.empty((n, d), device=dev) for _ in range(K - 1)]
     out_c = torch.empty((n, d), device=dev)
-    bufs = (ctypes.c_void_p * (K - 1))(*[t.data_ptr() for t in layers])
     e0 = engine.rows_desc(segs, d)
     P = engine._ptr
 
-    def c_host():
+    py_plans, _ = engine._side_plans(g, d, 128, "exact", None, True)
+
+    def c_host(pl=plans):
+        # fresh output buffers per call, as the Python binding allocates them (same allocator)
+        lay = [torch.empty((n, d), device=dev) for _ in range(K - 1)]
+        bf = (ctypes.c_void_p * (K - 1))(*[t.data_ptr() for t in lay])
+        out_c.data = torch.empty((n, d), device=dev)
         rc = lib.lgcn_propagate_forward_sides(
-            P(g.rowptr), P(g.edges), P(g.row_ids), ctypes.byref(sides), plans, e0, d, K, bufs,
+            P(g.rowptr), P(g.edges), P(g.row_ids), ctypes.byref(sides), pl, e0, d, K, bf,
             P(out_c), sc.handle, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert rc == 0, lib.lgcn_error_string(rc)
     out_py = [None]
@@ -71,14 +75,17 @@ def main():
     def python():
         out_py[0] = engine.propagate_forward(g, segs, K)
     # interleaved: box-to-box and run-to-run drift hits both sides alike
-    t_c, t_py = [], []
+    t_c, t_py, t_cp = [], [], []
     for _ in range(3):
         t_c.append(median_ms(c_host, reps))
         t_py.append(median_ms(python, reps))
-    t_c, t_py = float(np.median(t_c)), float(np.median(t_py))
+        t_cp.append(median_ms(lambda: c_host(py_plans), reps))
+    t_c, t_py, t_cp = (float(np.median(t)) for t in (t_c, t_py, t_cp))
+    c_host()
     same = bool(torch.equal(out_c, out_py[0]))
-    print(f"C host lgcn_propagate_forward_sides: {t_c:.3f} ms; engine.propagate_forward: "
-          f"{t_py:.3f} ms; ratio {t_c / t_py:.3f}; outputs bitwise equal: {same}", flush=True)
+    print(f"C host lgcn_propagate_forward_sides (C-planner plans): {t_c:.3f} ms; the same call "
+          f"with the Python binding's plans: {t_cp:.3f} ms; engine.propagate_forward: {t_py:.3f} "
+          f"ms; ratio C/Python {t_c / t_py:.3f}; outputs bitwise equal: {same}", flush=True)
 
 
 if __name__ == "__main__":

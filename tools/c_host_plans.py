@@ -68,5 +68,9 @@ def c_host_side_plans(lib, rowptr_host, row_ids_host, segments, nnz_total, d, de
                 bufs = [torch.empty(int(x), dtype=torch.uint8, device=device) for x in sz]
                 keep += bufs
                 p.emu_rel, p.emu_meta, p.emu_stage = (t.data_ptr() for t in bufs)
+            if base.n_emu_rows:  # the deferred mean's row sums (lgcn_hub_plan_t emu_out)
+                eo = torch.empty(base.n_emu_rows * d, dtype=torch.float32, device=device)
+                keep.append(eo)
+                p.emu_out = eo.data_ptr()
             plans[2 * g + j] = p
     return plans, keep

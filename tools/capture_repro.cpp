@@ -7,6 +7,8 @@
 //   nested — L forks A[i] and joins them back into L every half-layer (lane 1 with its own aux
 //            streams under a capture: LGCN_SCHED_CAPTURE_AUX=1), A[i] also joined into s at the
 //            end, as lgcn_engine.hip's join_lanes does
+// argv[3] (priorities, as engine.py creates lane 1's streams): "high" = L and A[i] created at
+// high priority, "aux" = A[i] only, default none
 // Every record uses its own event. Prints "replay ok" after capturing, instantiating and
 // launching the graph twice and checking the result; a crash in hipStreamEndCapture is the ROCm
 // behaviour the engine guards against.
@@ -34,11 +36,16 @@ __global__ void k_add(float* p, int n, float v) {
 int main(int argc, char** argv) {
     const bool nested = argc > 1 && strcmp(argv[1], "nested") == 0;
     const int layers = argc > 2 ? atoi(argv[2]) : 3;
+    const char* prio = argc > 3 ? argv[3] : "none";
+    const bool hi_l = strcmp(prio, "high") == 0, hi_a = hi_l || strcmp(prio, "aux") == 0;
+    int lo_p = 0, hi_p = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo_p, &hi_p));
     const int na = 3, n = 1 << 16;
     hipStream_t s, L, A[na];
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    CK(hipStreamCreateWithFlags(&L, hipStreamNonBlocking));
-    for (int i = 0; i < na; ++i) CK(hipStreamCreateWithFlags(&A[i], hipStreamNonBlocking));
+    CK(hipStreamCreateWithPriority(&L, hipStreamNonBlocking, hi_l ? hi_p : lo_p));
+    for (int i = 0; i < na; ++i)
+        CK(hipStreamCreateWithPriority(&A[i], hipStreamNonBlocking, hi_a ? hi_p : lo_p));
     std::vector<hipEvent_t> pool(512);
     for (auto& e : pool) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     size_t next = 0;
@@ -73,7 +80,8 @@ int main(int argc, char** argv) {
     }
     CK(link(L, s));
     for (int i = 0; i < na; ++i) CK(link(A[i], s));
-    printf("ending capture (%s, %d layers)\n", nested ? "nested" : "flat", layers);
+    printf("ending capture (%s, %d layers, priorities %s: %d..%d)\n", nested ? "nested" : "flat",
+           layers, prio, lo_p, hi_p);
     fflush(stdout);
     hipGraph_t g;
     CK(hipStreamEndCapture(s, &g));
