@@ -1018,15 +1018,22 @@ int wait_ev(hipStream_t st, hipEvent_t e) { return e ? herr(hipStreamWaitEvent(s
 // the parts fork and join with the rest and part_done fires with the joined layer.
 struct Deps {
     hipEvent_t late[3] = {nullptr, nullptr, nullptr};
+    // late_emu: operands only the emulated rows' epilogue reads (their own rows of the earlier
+    // layers, made by the other lane's walked parts): with a deferred epilogue only it waits for
+    // them, otherwise they count as `late`
+    hipEvent_t late_emu[2] = {nullptr, nullptr};
     hipEvent_t part_wait[2] = {nullptr, nullptr};
     bool defer = false;
     hipEvent_t part_done[2] = {nullptr, nullptr};
 };
 
-int wait_late(hipStream_t st, const Deps* dp) {
+int wait_late(hipStream_t st, const Deps* dp, bool emu = true) {
     if (!dp) return 0;
     for (hipEvent_t e : dp->late)
         if (int r = wait_ev(st, e)) return r;
+    if (emu)
+        for (hipEvent_t e : dp->late_emu)
+            if (int r = wait_ev(st, e)) return r;
     return 0;
 }
 
@@ -1105,7 +1112,8 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     // a MEAN whose operands arrive late (the other lane's layer K-1) with an emu_out scratch: the
     // walks and chains write their rows' sums there (LGCN_EPI_ROWS) without waiting for them, and
     // the mean of those rows follows on `s` once they are ready (lgcn_emu_epilogue)
-    const bool has_late = dp && (dp->late[0] || dp->late[1] || dp->late[2]);
+    const bool has_late = dp && (dp->late[0] || dp->late[1] || dp->late[2] ||
+                                 dp->late_emu[0] || dp->late_emu[1]);
     const bool defer_epi = sc && has_late && ep.mode == LGCN_EPI_MEAN && p.emu_out && ne > 0 &&
                            !live;
     lgcn_epilogue_t ep_rows;
@@ -1209,8 +1217,9 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
                 if (int e = mark(1 + i, aux_of(i))) return e;
         }
     // the block passes read X only; every kernel after them writes Y, whose epilogue operands
-    // are ready once `late` fires (the walks and chains write emu_out instead when deferred)
-    if (int e = wait_late(s, dp)) return e;
+    // are ready once `late` fires (the walks and chains write emu_out instead when deferred, and
+    // only their epilogue waits for late_emu)
+    if (int e = wait_late(s, dp, !defer_epi)) return e;
     if (!defer_epi)
         for (int i = 0; i < na; ++i)
             if (int e = wait_late(sc->aux[i], dp)) return e;
@@ -1239,8 +1248,11 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
             return e;
         }
     }
-    if (defer_epi)
+    if (defer_epi) {
+        for (hipEvent_t e : dp->late_emu)
+            if (int r = wait_ev(s, e)) return r;
         if (int e = lgcn_emu_epilogue(p.emu_rows, ne, p.emu_out, d, y, ldy, d, &ep, s)) return e;
+    }
     if (int e = mark(7, s)) return e;
     return own ? 0 : done_on_s();
 }
@@ -1438,10 +1450,10 @@ int run_sides(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* ro
                 dp.part_wait[1] = ab[k - 1];
             }
             dp.defer = k < K && sched && !cap;
-            if (mean && k >= 2) {
+            if (mean && k >= 2) {  // the layer kernel's rows read layer K-1's layer-kernel rows
                 dp.late[0] = rest[k - 1];
-                dp.late[1] = part[k - 1][0];
-                dp.late[2] = part[k - 1][1];
+                dp.late_emu[0] = part[k - 1][0];
+                dp.late_emu[1] = part[k - 1][1];
             }
             if (int e = seg_layer(rowptr, edges, row_ids, sd.split, n, plans, k, 3, io, d, sched,
                                   L, &dp))
