@@ -1009,6 +1009,8 @@ def _stream_priorities(n_aux):
         return [i in (0, 1, 4, 5) for i in range(n_aux)]
     if mode == "hub":   # lane 1's main + walked parts, and lane 0's part 0 (its longest walk)
         return [i in (0, 3, 4, 5) for i in range(n_aux)]
+    if mode == "aux1":  # lane 1's aux streams only (its layer kernels at normal priority)
+        return [i in (4, 5, 6) for i in range(n_aux)]
     return [i >= 3 for i in range(n_aux)]
 
 

@@ -70,10 +70,28 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--bursts", type=int, default=-3, help="show the last N bursts (negative)")
     ap.add_argument("--all", action="store_true", help="every dispatch, not grouped")
+    ap.add_argument("--sum", action="store_true",
+                    help="per kernel name: dispatches, summed duration, first start / last end")
     a = ap.parse_args()
     bs = bursts(load(a.dir))
     for b in bs[a.bursts:]:
-        show(b, a.all)
+        if a.sum:
+            t0 = b[0][0]
+            agg = defaultdict(lambda: [0, 0, None, 0])
+            for st, en, name, _, _ in b:
+                g = agg[name]
+                g[0] += 1
+                g[1] += en - st
+                g[2] = st if g[2] is None else min(g[2], st)
+                g[3] = max(g[3], en)
+            span = (max(r[1] for r in b) - t0) / 1e6
+            print(f"burst: {len(b)} dispatches, {span:.3f} ms, kernel time "
+                  f"{sum(g[1] for g in agg.values()) / 1e6:.3f} ms")
+            for name, (cnt, tot, f, l) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+                print(f"  n={cnt:4d} sum {tot / 1e6:8.3f}  [{(f - t0) / 1e6:7.3f} -> "
+                      f"{(l - t0) / 1e6:7.3f}]  {name[:110]}")
+        else:
+            show(b, a.all)
 
 
 if __name__ == "__main__":
