@@ -208,13 +208,45 @@ def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
     for b in batches[:4]:
         step(b)
     torch.cuda.synchronize()
+    retries0 = torch.cuda.memory_stats(dev).get("num_alloc_retries", 0)
     a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_host = time.time()
     a.record()
     for b in batches[4:]:
         loss = step(b)
     e.record()
+    t_host = (time.time() - t_host) * 1e3 / args.train_steps
     torch.cuda.synchronize()
     ms = a.elapsed_time(e) / args.train_steps
+    retries = torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) - retries0
+    if os.environ.get("BENCH_PROFILE_TRAIN"):  # host profile of 2 steps (diagnostics, to stderr)
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for b in batches[:2]:
+            step(b)
+        pr.disable()
+        torch.cuda.synchronize()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(20)
+    # where a step's time goes: forward + loss, backward, optimizer, each bracketed by events on
+    # the current stream (3 more steps; the events sit between the phases, no host sync inside)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    phases = np.zeros(3)
+    for b in batches[:3]:
+        users, pos, neg = b
+        ev[0].record()
+        opt.zero_grad()
+        fu, fi, fb, u0, i0 = model(adj, use_brand=False)
+        loss_ = bpr_loss_reg(fu[users], fi[pos], fi[neg], u0[users], i0[pos], i0[neg], 1e-4)
+        ev[1].record()
+        loss_.backward()
+        ev[2].record()
+        opt.step()
+        ev[3].record()
+        torch.cuda.synchronize()
+        phases += [ev[i].elapsed_time(ev[i + 1]) for i in range(3)]
+    phases /= 3
     # the same loop with torch's fused Adam (one kernel per parameter instead of main.py's
     # default foreach Adam, ~16 ms of multi_tensor_apply launches at C3): what the step costs
     # when the optimizer is not the bottleneck
@@ -233,6 +265,10 @@ def bench_train_step(adj, emb_host, U, I, d, K, dev, args):
            "batch": 2048, "optimizer": "Adam(lr=1e-3) (main.py's default: foreach)",
            "loss_last": float(loss.item()),
            "fused_adam_ms_per_step": round(ms_fused, 3),
+           "phases_ms": {"forward_and_loss": round(float(phases[0]), 3),
+                         "backward": round(float(phases[1]), 3),
+                         "adam": round(float(phases[2]), 3)},
+           "host_enqueue_ms_per_step": round(t_host, 3), "alloc_retries": int(retries),
            "what": f"main.py:488-531 hot loop: forward + gathers + bpr_loss_reg + backward + "
                    f"Adam over all {U + I:,} x {d} parameters; fused_adam_ms_per_step: the same "
                    f"with torch.optim.Adam(fused=True)"}

@@ -1223,7 +1223,8 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     if (!defer_epi)
         for (int i = 0; i < na; ++i)
             if (int e = wait_late(sc->aux[i], dp)) return e;
-    // the layer kernel waits for part 0's block pass
+    // the layer kernel waits for part 0's block pass (round 5: the mean half-layers without this
+    // wait measured the same, 12.40 / 12.68 vs 12.38 / 12.64 ms)
     if (parts[0].b1 > parts[0].b0)
         if (int e = link(sc, aux_of(0), s)) return e;
     if (int e = layer_kernel(s)) return e;

@@ -1403,6 +1403,10 @@ int lgcn_emu_blocks(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, in
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int4* mp = static_cast<int4*>(meta);
     int4* kp = reinterpret_cast<int4*>(rel);
+#ifdef LGCN_EXP_NOSTAGE  // timing experiment only (wrong results): no stage writes after N calls
+    static int calls = 0;
+    if (++calls > LGCN_EXP_NOSTAGE) stage = nullptr;
+#endif
 #define LGCN_B(XD_) \
     case XD_: return launch_blocks<XD_>(edges, blocks, n_blocks, x, xa, x_nz, d, kp, mp, stage, live, s);
     switch (xd) {

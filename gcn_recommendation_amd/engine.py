@@ -1011,6 +1011,8 @@ def _stream_priorities(n_aux):
         return [i in (0, 3, 4, 5) for i in range(n_aux)]
     if mode == "aux1":  # lane 1's aux streams only (its layer kernels at normal priority)
         return [i in (4, 5, 6) for i in range(n_aux)]
+    if mode == "lane0":  # lane 0's aux streams (its layer kernels run on the caller's stream)
+        return [i in (0, 1, 2) for i in range(n_aux)]
     return [i >= 3 for i in range(n_aux)]
 
 
