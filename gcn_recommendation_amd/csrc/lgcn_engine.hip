@@ -1713,6 +1713,8 @@ int lgcn_propagate_backward_sides(const int32_t* rowptr, const lgcn_edge_t* edge
         io.ep.div = (float)(K + 1);
         return io;
     };
+    // (round 5: the backward with its lanes flipped, the high-priority lane carrying the chain
+    // of half-layers that starts with side 0, measured 9.74 / 9.76 vs 9.65 / 9.64 ms: not kept)
     return run_sides(rowptr, edges, row_ids, *sides, plans, d, K, layer, sched, s);
 }
 

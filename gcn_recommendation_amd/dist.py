@@ -425,6 +425,7 @@ def featsplit_train_timing(plan, x_slot, K, args, dev, hub_thr, batch=2048):
         loss = bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
         loss.backward()
         opt.step()
+        loss.item()  # main.py:527 reads the loss back every batch
         return [] if timed else None
     ms, _ = _timed(step, args.train_steps, 2, dev)
     (ms_max,) = _max_over_ranks(torch.tensor([ms / args.train_steps], dtype=torch.float64,
@@ -483,6 +484,40 @@ def profiled_traffic(cfg, args, mode, d_rank):
     return None
 
 
+def _sided_store_launches(graph, x_slot, K, hub_thr, hub_mode, d, run, steps):
+    """(ms per STORE layer-kernel segment launch, algorithmic bytes per launch) of a sided graph:
+    `steps` calls of run() with engine.side_timing on (each segment's layer kernel timed on its
+    lane's stream), bytes = the SURVEY 8d model over the rows the layer kernel runs (bundle rows
+    and, in the exact plan, whole-row items up to emu_min_degree), as bench.py's N = 1 line."""
+    engine.side_timing = []
+    try:
+        for _ in range(steps):
+            run()
+        torch.cuda.synchronize()
+        tm = engine.side_timing
+    finally:
+        engine.side_timing = None
+    ker = np.array([[[t[(k, g)][0].elapsed_time(t[(k, g)][1]) if (k, g) in t else 0.0
+                      for g in range(engine.N_SEGS)] for k in range(1, K + 1)] for t in tm])
+    rp = graph.rowptr_host().astype(np.int64)
+    emu_min = engine.emu_min_degree_from_env(graph.nnz)
+    thr = min(hub_thr if hub_thr is not None else engine.hub_threshold_from_env(),
+              engine.INT32_MAX)
+    cut = max(thr, emu_min if hub_mode == "exact" else 0)
+
+    def kernel_bytes(a, b):
+        deg = np.diff(rp[a:b + 1])
+        run_ = deg <= cut
+        return int(deg[run_].sum()) * (4 * d + 8) + 4 * (b - a + 1) + 4 * int(run_.sum()) * d
+    segs = graph.segments()
+    live = [g for g, (a, b) in enumerate(segs) if b > a]
+    st = ker[:, :-1, :] if K > 1 else ker
+    n_launch = max(len(live) * st.shape[1], 1)
+    store_ms = float(st.sum(axis=(1, 2)).mean()) / n_launch
+    b_launch = sum(kernel_bytes(*segs[g]) for g in live) * st.shape[1] / n_launch
+    return store_ms, b_launch
+
+
 def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     rank, world = init("cuda")
     d, K = cfg["d"], cfg["K"]
@@ -536,11 +571,23 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
     ms, lay = _timed(fn, args.steps, args.warmup, dev)
     if lay.shape[1] == 1 and K > 1:  # sided featsplit: whole steps; a layer's share of one
         lay = np.repeat(lay / K, K, axis=1)
-    t = torch.tensor([ms, float(lay[:, :-1].mean() if K > 1 else lay.mean()), float(lay.mean())],
-                     dtype=torch.float64, device=dev)
+    hub_mode = engine.hub_mode_from_env()
+    if mode == "featsplit" and sided:
+        # the N = 1 line's basis (bench.py): the STORE layer-kernel segment launches, each timed on
+        # its lane's stream in a second loop, algorithmic bytes over the rows the kernel runs
+        store_ms, b_layer = _sided_store_launches(plan.graph, x_slot, K, hub_thr, hub_mode, dl,
+                                                  lambda: plan.forward(x_slot, K, hub_thr),
+                                                  min(args.steps, 5))
+        basis = ("algorithmic bytes (SURVEY 8d) of the rows the layer kernel runs / its segment "
+                 "launch time (STORE layers 1..K-1, each timed on its lane's stream), per GPU, "
+                 "max over ranks — the N = 1 line's basis")
+    else:
+        store_ms = float(lay[:, :-1].mean() if K > 1 else lay.mean())
+        basis = "algorithmic bytes (SURVEY 8d) / whole-layer time (store layers), per GPU, " \
+                "max over ranks"
+    t = torch.tensor([ms, store_ms, float(lay.mean())], dtype=torch.float64, device=dev)
     ms_max, kern_ms, all_ms = _max_over_ranks(t)
     c4 = rp = bwd = chunk = None
-    hub_mode = engine.hub_mode_from_env()
     if mode == "featsplit" and hub_mode == "exact":
         # secondary: the same shard forward with chunked hub rows (fixed-order partial sums, not
         # the reference's rounding on hub rows): the throughput the split gets when the
@@ -564,6 +611,10 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
         rp = rowpart_secondary(r, c, v, n, nnz, K, d, emb_host, world, rank, args, dev, hub_thr)
     value = K * nnz * args.steps / (ms_max / 1e3)
     achieved = b_layer / (kern_ms / 1e3) / 1e9
+    dw = dl if mode == "featsplit" else d
+    b_fwd = K * (nnz * (4 * dw + 8) + 4 * (n + 1) + 4 * n * dw) if mode == "featsplit" else \
+        K * b_layer
+    fwd_rate = b_fwd / (ms_max / args.steps / 1e3) / 1e9
     return {
         "metric": "propagated edges/sec (SpMM) + Recall@20, Amazon-Books 3-layer d=64",
         "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
@@ -577,8 +628,11 @@ def bench_distributed(args, cfg, r, c, v, emb_host, dev, hub_thr):
                    "exchange_bytes_per_step_per_rank": int(comm), **extra},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
                      "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
-                     "basis": "algorithmic bytes (SURVEY 8d) / whole-layer time (store layers), "
-                              "per GPU, max over ranks; no PMC pass of this build at N > 1",
+                     "basis": basis + "; no PMC pass of this build at N > 1",
+                     "forward": {"bytes": int(b_fwd), "achieved": round(fwd_rate, 1),
+                                 "frac": round(fwd_rate / 8000.0, 4),
+                                 "note": "the rank's K x SURVEY 8d bytes per forward / "
+                                         "ms_per_step (as the N = 1 line's roofline.forward)"},
                      "round1_pmc_traffic_chunk_mode": profiled_traffic(
                          cfg, args, mode, d // world if mode == "featsplit" else None),
                      "kernel": "k_layer store layers, per GPU (max over ranks)",
