@@ -994,25 +994,12 @@ def _side_stream(device, i=0, high=False):
 def _stream_priorities(n_aux):
     """Which auxiliary streams run at high priority. One lane (n_aux <= 3): aux 0, the longest
     rows' walks (a layer's critical path). Two lanes: all of lane 1 (aux 3 = its main stream and
-    aux 4..6) — it carries the chain of half-layers ending in layer K's items, the propagation's
-    critical path (lgcn_propagate_*_sides); LGCN_LANE_PRIORITY=part0 instead raises each lane's
-    part-0 stream (aux 0 and 4), =parts both lanes' walked parts (aux 0, 1, 4, 5: the latency-bound
-    block passes and walks), leaving the layer kernels and chains of both lanes at normal
-    priority, =hub lane 1 but its chains, plus lane 0's part 0 (aux 0, 3, 4, 5) (4 + 4 streams:
-    one hardware queue each under HIP's default)."""
+    aux 4..6) — 4 + 4 streams: one hardware queue each under HIP's default 4 per priority.
+    Measured at C3 against: no priorities, lane 0's aux streams, both
+    lanes' part-0 streams, lane 1's layer kernels or its chains at normal priority (with 8
+    queues per priority) — none faster, most slower."""
     if n_aux <= 3:
         return [i == 0 for i in range(n_aux)]
-    mode = os.environ.get("LGCN_LANE_PRIORITY", "lane1")
-    if mode == "part0":
-        return [i in (0, 4) for i in range(n_aux)]
-    if mode == "parts":
-        return [i in (0, 1, 4, 5) for i in range(n_aux)]
-    if mode == "hub":   # lane 1's main + walked parts, and lane 0's part 0 (its longest walk)
-        return [i in (0, 3, 4, 5) for i in range(n_aux)]
-    if mode == "aux1":  # lane 1's aux streams only (its layer kernels at normal priority)
-        return [i in (4, 5, 6) for i in range(n_aux)]
-    if mode == "lane0":  # lane 0's aux streams (its layer kernels run on the caller's stream)
-        return [i in (0, 1, 2) for i in range(n_aux)]
     return [i >= 3 for i in range(n_aux)]
 
 
@@ -1082,7 +1069,7 @@ def sched_for(device, n_aux=None):
     if not emu_overlap_enabled():
         return None
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_LANE_PRIORITY", ""), os.environ.get("LGCN_SCHED_CLASSES", ""),
+           os.environ.get("LGCN_SCHED_CLASSES", ""),
            os.environ.get("LGCN_CAPTURE_AUX", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
