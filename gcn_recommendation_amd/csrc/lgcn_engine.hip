@@ -976,7 +976,6 @@ struct lgcn_sched {
     hipEvent_t* trace_sides;   // optional [32 K] (LGCN_SCHED_TRACE_SIDES)
     hipEvent_t* timing_sides;  // optional [8 K] (LGCN_SCHED_TIMING_SIDES)
     int classes;               // LGCN_SCHED_CLASSES (default 1)
-    int capture_aux;           // LGCN_SCHED_CAPTURE_AUX (default 0)
 };
 
 namespace {
@@ -1272,15 +1271,20 @@ bool capturing(hipStream_t s) {
 
 // The two lanes: lane 1 on its own streams when the schedule has them, else both lanes share
 // the caller's stream (half-layers then run in layer order, each still overlapped inside).
-// While `s` is being captured, lane 1 runs its half-layers on its main stream alone unless
-// LGCN_SCHED_CAPTURE_AUX = 1 (rounds 3-4: a capture that forked lane 1's own aux streams crashed
-// hipStreamEndCapture while one fork/join event was re-recorded across the half-layers of a
-// call; every record now has its own event).
+// While `s` is being captured, lane 1 runs its half-layers on its main stream alone: a capture
+// that forks lane 1's own aux streams crashes hipStreamEndCapture on this ROCm (rounds 3-5,
+// with every record on its own event too, while a plain-HIP replay of the same
+// stream/event sequence captures fine). The diagnostic build LGCN_CAPTURE_AUX_EXP keeps them.
+#ifdef LGCN_CAPTURE_AUX_EXP
+constexpr bool kCaptureAux = true;
+#else
+constexpr bool kCaptureAux = false;
+#endif
 bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2], bool& l1_aux) {
     lanes[0] = Lane{s, sc};
     const bool two = sc && sc->lane1;
     const bool cap = capturing(s);
-    l1_aux = two && sc->lane1->n_aux > 0 && (!cap || sc->capture_aux);
+    l1_aux = two && sc->lane1->n_aux > 0 && (!cap || kCaptureAux);
     lanes[1] = two ? Lane{sc->lane1_main, l1_aux ? sc->lane1 : nullptr} : lanes[0];
     if (sc) {
         sc->pool->state[0] = two ? 2 : 1;
@@ -1510,7 +1514,6 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
     sc->n_aux = n0;
     sc->chain = 1;
     sc->classes = 1;
-    sc->capture_aux = 0;
     for (int i = 0; i < n0; ++i) sc->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[i]);
     int e = 0;
     for (; pool->n < kPoolEvents && !e; ++pool->n)
@@ -1527,7 +1530,6 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
             l1->n_aux = n_aux - 4;
             l1->chain = 1;
             l1->classes = 1;
-            l1->capture_aux = 0;
             for (int i = 0; i < l1->n_aux; ++i)
                 l1->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[4 + i]);
         }
@@ -1581,9 +1583,6 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
             return 0;
         case LGCN_SCHED_CLASSES:
             sc->classes = value != 0;
-            return 0;
-        case LGCN_SCHED_CAPTURE_AUX:
-            sc->capture_aux = value != 0;
             return 0;
         default:
             return LGCN_EINVAL;

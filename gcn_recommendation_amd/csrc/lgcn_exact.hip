@@ -264,20 +264,26 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
         }
     };
     int2 rec = load_rec(blk.beg);
+    float xa[SW], va[SW], xb[SW], vb[SW];
+    // the loads of sub-window k + 1 are issued before sub-window k is computed — across the
+    // 64-edge windows too: the last sub-window of a window is computed while the next window's
+    // first sub-window is in flight (its records were loaded at the window's start)
+    load_sub(rec, 0, min(64, blk.end - blk.beg), xa, va);
     for (int32_t j0 = blk.beg; j0 < blk.end; j0 += 64) {
         const int n = min(64, blk.end - j0);
+        const bool more = j0 + 64 < blk.end;
         const int2 nrec = load_rec(j0 + 64);  // next window's records, in flight meanwhile
         if (sv) sv[j0 - blk.beg + lane] = __int_as_float(rec.y);  // (0 past the block end)
-        float xa[SW], va[SW], xb[SW], vb[SW];
         const int w0 = j0 - blk.beg;
-        // the loads of sub-window k + 1 are issued before sub-window k is computed
-        load_sub(rec, 0, n, xa, va);
 #pragma unroll
         for (int k = 0; k < 64 / SW; k += 2) {
             load_sub(rec, (k + 1) * SW, n, xb, vb);
             run_sub(xa, va);
             stage_sub(xa, k % (32 / SW));
-            if (k + 2 < 64 / SW) load_sub(rec, (k + 2) * SW, n, xa, va);
+            if (k + 2 < 64 / SW)
+                load_sub(rec, (k + 2) * SW, n, xa, va);
+            else if (more)  // (round 5: 12.98 / 13.07 vs 13.04 / 13.29 ms forward, A/B)
+                load_sub(nrec, 0, min(64, blk.end - j0 - 64), xa, va);
             run_sub(xb, vb);
             stage_sub(xb, (k + 1) % (32 / SW));
             if ((k + 2) % (32 / SW) == 0) stage_flush(w0 + (k + 2 - 32 / SW) * SW);

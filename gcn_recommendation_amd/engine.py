@@ -28,7 +28,7 @@ TUNE_EMU_MARGIN = 6
 SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, SCHED_TRACE = \
     1, 2, 3, 4, 5, 6
 SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
-SCHED_CLASSES, SCHED_CAPTURE_AUX = 16, 17
+SCHED_CLASSES = 16
 SCHED_STATE_LANES, SCHED_STATE_L1_AUX, SCHED_STATE_CAPTURING, SCHED_STATE_CLASSES = 1, 2, 3, 4
 # segments of a sided propagation: the three side-0 classes, then side 1
 N_SEGS = 4
@@ -1043,9 +1043,8 @@ class Sched:
         self.set(SCHED_SLOTS1, slots[min(1, len(slots) - 1)])
         self.set(SCHED_CHAIN, 1 if chain_enabled() else 0)
         # LGCN_SCHED_CLASSES=0: the walked parts of side 1 wait for the whole side-0 half-layer
-        # (A/B; same bits); LGCN_CAPTURE_AUX=1: lane 1 keeps its aux streams under a capture
+        # (A/B; same bits)
         self.set(SCHED_CLASSES, 0 if os.environ.get("LGCN_SCHED_CLASSES", "1") == "0" else 1)
-        self.set(SCHED_CAPTURE_AUX, 1 if os.environ.get("LGCN_CAPTURE_AUX", "0") == "1" else 0)
 
     def state(self, what):
         """lgcn_sched_state: what the latest sided call on this schedule ran."""
@@ -1069,8 +1068,7 @@ def sched_for(device, n_aux=None):
     if not emu_overlap_enabled():
         return None
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_SCHED_CLASSES", ""),
-           os.environ.get("LGCN_CAPTURE_AUX", ""))
+           os.environ.get("LGCN_SCHED_CLASSES", ""))
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1])
     return _scheds[key]

@@ -495,9 +495,7 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        and lets side 1's walked parts wait only for the classes
                                        they read (lgcn_sides_t); 0: every part waits for the
                                        whole side-0 half-layer before it (same bits) */
-#define LGCN_SCHED_CAPTURE_AUX  17  /* 1: lane 1 keeps its aux streams while the caller's stream
-                                       is being captured into a HIP graph; 0 (default): lane 1 runs
-                                       its half-layers on its main stream alone under a capture */
+/* (under a HIP-graph capture lane 1 runs its half-layers on its main stream alone: DESIGN §4d) */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 /* What the latest lgcn_propagate_*_sides call on this schedule ran (diagnostics, tests). */
 #define LGCN_SCHED_STATE_LANES     1  /* 2: two lanes, 1: one */

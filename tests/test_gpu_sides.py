@@ -148,7 +148,7 @@ def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):
     x = [t.detach() for t in w]
     cap = engine.CapturedForward(g, x, 3, hub_threshold=128)
     # the capture ran the two lanes (lane 1 without its own aux streams: the library's default
-    # under a capture, LGCN_SCHED_CAPTURE_AUX)
+    # under a capture: DESIGN §4d)
     s = engine.last_schedule
     assert (s["lanes"], s["lane1_aux"], s["captured"], s["aux_streams"]) == (2, 0, True, 7)
     for _ in range(2):
@@ -227,31 +227,6 @@ def test_default_environment_runs_two_lanes(gpu_device, monkeypatch, brand_graph
     assert (s["lanes"], s["lane1_aux"], s["captured"], s["aux_streams"]) == (2, 3, False, 7)
     got = torch.cat([o.detach() for o in out]).cpu().numpy()
     assert np.array_equal(got, oracle.forward(r, c, v, e0, 3))
-
-
-@pytest.mark.parametrize("K", [3, 4])
-def test_capture_with_lane1_aux_streams(gpu_device, monkeypatch, brand_graph, K):
-    """LGCN_SCHED_CAPTURE_AUX = 1: the captured forward forks lane 1's own aux streams too (every
-    event record of a call on its own event), all three classes populated; replays bitwise,
-    inputs updated in place are seen."""
-    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
-    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
-    monkeypatch.setenv("LGCN_CAPTURE_AUX", "1")
-    _classes_env(monkeypatch, "on")
-    r, c, v, n = brand_graph
-    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
-    rng = np.random.default_rng(17)
-    e0 = _e0(rng, "xavier", n, 64)
-    x = _segs(e0, gpu_device)
-    cap = engine.CapturedForward(g, x, K, hub_threshold=128)
-    s = engine.last_schedule
-    # (under a capture every half-layer joins its parts: no class dependencies, lgcn_engine.hip)
-    assert (s["lanes"], s["lane1_aux"], s["captured"], s["classes"]) == (2, 3, True, False)
-    assert np.array_equal(cap.replay().cpu().numpy(), oracle.forward(r, c, v, e0, K))
-    e1 = _e0(rng, "xavier", n, 64)
-    for t, a in zip(x, _segs(e1, gpu_device)):
-        t.copy_(a)
-    assert np.array_equal(cap.replay().cpu().numpy(), oracle.forward(r, c, v, e1, K))
 
 
 @pytest.mark.parametrize("classes", ["on", "graph_off"])

@@ -5,7 +5,7 @@
 //   flat   — the aux streams are forked from s and joined into s only (the engine's default
 //            under a capture: lane 1 runs on L alone, lane 0's aux streams fork from s)
 //   nested — L forks A[i] and joins them back into L every half-layer (lane 1 with its own aux
-//            streams under a capture: LGCN_SCHED_CAPTURE_AUX=1), A[i] also joined into s at the
+//            streams under a capture: the library built with LGCN_CAPTURE_AUX_EXP), A[i] also joined into s at the
 //            end, as lgcn_engine.hip's join_lanes does
 // argv[3] (priorities, as engine.py creates lane 1's streams): "high" = L and A[i] created at
 // high priority, "aux" = A[i] only, default none
