@@ -991,7 +991,7 @@ def _side_stream(device, i=0, high=False):
     return sc[(i, high)]
 
 
-def _stream_priorities(n_aux):
+def _stream_priorities(n_aux, role="forward"):
     """Which auxiliary streams run at high priority. One lane (n_aux <= 3): aux 0, the longest
     rows' walks (a layer's critical path). Two lanes: all of lane 1 (aux 3 = its main stream and
     aux 4..6) — 4 + 4 streams: one hardware queue each under HIP's default 4 per priority.
@@ -1000,6 +1000,8 @@ def _stream_priorities(n_aux):
     queues per priority) — none faster, most slower."""
     if n_aux <= 3:
         return [i == 0 for i in range(n_aux)]
+    if role == "backward":
+        return [False] * n_aux
     return [i >= 3 for i in range(n_aux)]
 
 
@@ -1028,11 +1030,11 @@ class Sched:
     """lgcn_sched_t over this device's side streams (created once per device and stream count;
     the C library owns the fork/join events). n_aux >= 4: two lanes (lgcn_propagate_*_sides)."""
 
-    def __init__(self, device, n_aux):
+    def __init__(self, device, n_aux, role="forward"):
         lib = load_library()
         self.lib, self.device, self.n_aux = lib, device, n_aux
         self.streams = [_side_stream(device, i, hi)
-                        for i, hi in enumerate(_stream_priorities(n_aux))]
+                        for i, hi in enumerate(_stream_priorities(n_aux, role))]
         arr = (ctypes.c_void_p * n_aux)(*[st.cuda_stream for st in self.streams])
         h = ctypes.c_void_p()
         with torch.cuda.device(device):
@@ -1061,16 +1063,18 @@ class Sched:
             pass
 
 
-def sched_for(device, n_aux=None):
+def sched_for(device, n_aux=None, role="forward"):
     """The device's Sched (None with LGCN_EMU_OVERLAP=0: every part in order on the caller's
     stream). n_aux: default n_aux_streams(). Made outside any capture on first use (the C
     library creates its events there; a captured call reuses them)."""
     if not emu_overlap_enabled():
         return None
+    if role == "backward" and os.environ.get("LGCN_BWD_NORMAL", "0") != "1":
+        role = "forward"
     key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_SCHED_CLASSES", ""))
+           os.environ.get("LGCN_SCHED_CLASSES", ""), role)
     if key not in _scheds:
-        _scheds[key] = Sched(device, key[1])
+        _scheds[key] = Sched(device, key[1], role)
     return _scheds[key]
 
 
@@ -1378,7 +1382,7 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         if use_sides(gt):
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
                                    live=nz is not None)
-            sc = sched_for(dev)
+            sc = sched_for(dev, role="backward")
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             sides = gt.sides_struct()
             try:
