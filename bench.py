@@ -908,7 +908,9 @@ def main():
         ms_c, lay_c, ker_c, out_c = timed("chunk", args.steps, 1)
         pc = parity(out_c.cpu().numpy())
         del out_c
-        store_c = float(ker_c[:, :-1].mean())
+        # per STORE layer: the layer kernel's launches (sided: one per segment, summed)
+        store_c = float(ker_c[:, :-1].sum(axis=2).mean() if ker_c.ndim == 3
+                        else ker_c[:, :-1].mean())
         b_full = nnz * (4 * d + 8) + 4 * (n + 1) + 4 * n * d  # every row runs in the kernel
         alg_c = b_full / (store_c / 1e3) / 1e9
         roof_c = {"bound": "hbm", "achieved": round(alg_c, 1), "peak": PEAK_HBM_GBS,
