@@ -1152,15 +1152,26 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
         if (int e = wait_late(s, dp)) return e;
     }
     if (live && sc) {
-        // aux[0]: the live-edge pass (its row flags gate the walks), then part 0's walk; aux[1]
-        // (after the flags): part 1
+        // aux[0]: the live-edge flags (they gate the walks), then part 0's block pass + walk;
+        // aux[1] (after the flags): part 1; aux[2] (after the flags): the live-edge chains —
+        // beside the walks rather than before them (a dense G keeps every walked row walked and
+        // makes every chain row a chain over all its edges: round 5, the dense backward's first
+        // layer no longer waits for its chains before its walks start)
         const int na = sc->n_aux;
-        hipStream_t a0 = sc->aux[0], a1 = sc->aux[na > 1 ? 1 : 0];
+        hipStream_t a0 = sc->aux[0], a1 = sc->aux[na > 1 ? 1 : 0], a2 = sc->aux[na > 2 ? 2 : 0];
         if (int e = mark(0, s)) return e;
         if (int e = link(sc, s, a0)) return e;
-        if (int e = live_rows(a0)) return e;
-        if (int e = mark(4, a0)) return e;
-        if (a1 != a0)
+        if (int e = lgcn_detail::live_prepare(edges, p.emu_blocks, p.n_emu_blocks, p.emu_rows, ne,
+                                              x_nz, d, xdiv, &ep, y, ldy, x.p0,
+                                              p.emu_part_rows[1], LGCN_LIVE_MAX, p.emu_live, a0))
+            return e;
+        if (a2 != a0)
+            if (int e = link(sc, a0, a2)) return e;
+        if (int e = lgcn_detail::live_chains(p.n_emu_blocks, ne, x, xdiv, y, ldy, d, &ep,
+                                             p.emu_live, a2))
+            return e;
+        if (int e = mark(4, a2)) return e;
+        if (a1 != a0 && a1 != a2)
             if (int e = link(sc, a0, a1)) return e;
         if (int e = walked(0, a0)) return e;
         if (int e = mark(5, a0)) return e;
@@ -1171,6 +1182,8 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
         if (int e = link(sc, a0, s)) return e;
         if (a1 != a0)
             if (int e = link(sc, a1, s)) return e;
+        if (a2 != a0 && a2 != a1)
+            if (int e = link(sc, a2, s)) return e;
         if (int e = mark(7, s)) return e;
         return done_on_s();
     }

@@ -47,6 +47,15 @@
 
 namespace lgcn_detail {
 extern int g_emu_margin;   // LGCN_TUNE_EMU_MARGIN (lgcn_engine.hip)
+// (declared for lgcn_engine.hip in lgcn_kernels.h; defined at the end of this file)
+int live_prepare(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                 const lgcn_emu_row_t* rows, int32_t n_rows, const uint32_t* x_nz, int32_t d,
+                 float x_div, const lgcn_epilogue_t* epi_host, float* y, int64_t ldy,
+                 const void* x_p0, int32_t live_min, int32_t max_live, void* scratch,
+                 hipStream_t s);
+int live_chains(int32_t n_blocks, int32_t n_rows, lgcn_rows_t x, float x_div, float* y,
+                int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* scratch,
+                hipStream_t s);
 }
 
 namespace {
@@ -1561,17 +1570,32 @@ int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int
                    const uint32_t* x_nz, float* y, int64_t ldy, int32_t d,
                    const lgcn_epilogue_t* epi_host, int32_t live_min, int32_t max_live,
                    void* scratch, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (int e = lgcn_detail::live_prepare(edges, blocks, n_blocks, rows, n_rows, x_nz, d, x_div,
+                                          epi_host, y, ldy, x.p0, live_min, max_live, scratch, s))
+        return e;
+    return lgcn_detail::live_chains(n_blocks, n_rows, x, x_div, y, ldy, d, epi_host, scratch, s);
+}
+
+}  // extern "C"
+
+namespace lgcn_detail {
+
+int live_prepare(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                 const lgcn_emu_row_t* rows, int32_t n_rows, const uint32_t* x_nz, int32_t d,
+                 float x_div, const lgcn_epilogue_t* epi_host, float* y, int64_t ldy,
+                 const void* x_p0, int32_t live_min, int32_t max_live, void* scratch,
+                 hipStream_t s) {
     if (n_rows < 0 || n_blocks < 0 || !lgcn_chain_supported(d) || d > 2048 || !x_nz ||
         !(x_div > 0.f) || !epi_host)
         return LGCN_EINVAL;
     if (n_rows == 0) return 0;
-    if (!edges || !blocks || !rows || !y || !scratch || ldy < d || !x.p0 || n_blocks < n_rows)
+    if (!edges || !blocks || !rows || !y || !scratch || ldy < d || !x_p0 || n_blocks < n_rows)
         return LGCN_EINVAL;
     // compacted spans are indexed by first_block * LGCN_EMU_BLOCK in int32 edge offsets
     if ((int64_t)n_blocks * LGCN_EMU_BLOCK > INT32_MAX) return LGCN_EINVAL;
     if (reinterpret_cast<uintptr_t>(scratch) & 255) return LGCN_EALIGN;
     const LiveScratch ls = live_layout(scratch, n_rows, n_blocks);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_live_count, dim3((uint32_t)n_blocks), dim3(64), 0, s, edges, blocks, x_nz,
                        ls.off);
     if (int e = herr_x(hipGetLastError())) return e;
@@ -1580,9 +1604,16 @@ int lgcn_live_rows(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int
     if (int e = herr_x(hipGetLastError())) return e;
     hipLaunchKernelGGL(k_live_scatter, dim3((uint32_t)n_blocks), dim3(64), 0, s, edges, blocks,
                        rows, x_nz, ls.off, ls.lrows, ls.ledges);
-    if (int e = herr_x(hipGetLastError())) return e;
-    return lgcn_chain_rows(ls.ledges, ls.lblocks, ls.lrows, n_rows, x, x_div, y, ldy, d, epi_host,
-                           stream);
+    return herr_x(hipGetLastError());
 }
 
-}  // extern "C"
+int live_chains(int32_t n_blocks, int32_t n_rows, lgcn_rows_t x, float x_div, float* y,
+                int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* scratch,
+                hipStream_t s) {
+    if (n_rows <= 0) return n_rows < 0 ? LGCN_EINVAL : 0;
+    const LiveScratch ls = live_layout(scratch, n_rows, n_blocks);
+    return lgcn_chain_rows(ls.ledges, ls.lblocks, ls.lrows, n_rows, x, x_div, y, ldy, d, epi_host,
+                           s);
+}
+
+}  // namespace lgcn_detail

@@ -47,6 +47,17 @@ int layer_mean(const LayerArgs& a);        // lgcn_layer_mean.hip
 int layer_add(const LayerArgs& a, int xd);         // lgcn_layer_add.hip
 int layer_add_div(const LayerArgs& a, int xd);     // lgcn_layer_add_div.hip
 int layer_add_sparse(const LayerArgs& a, int xd);  // lgcn_layer_add_sparse.hip
+// lgcn_live_rows in two steps (lgcn_exact.hip): the live-edge flags and compaction, then the
+// chains over the compacted live edges — so a schedule can run the chains on a stream of their
+// own once the flags (which gate the walks) are done
+int live_prepare(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks, int32_t n_blocks,
+                 const lgcn_emu_row_t* rows, int32_t n_rows, const uint32_t* x_nz, int32_t d,
+                 float x_div, const lgcn_epilogue_t* epi_host, float* y, int64_t ldy,
+                 const void* x_p0, int32_t live_min, int32_t max_live, void* scratch,
+                 hipStream_t s);
+int live_chains(int32_t n_blocks, int32_t n_rows, lgcn_rows_t x, float x_div, float* y,
+                int64_t ldy, int32_t d, const lgcn_epilogue_t* epi_host, void* scratch,
+                hipStream_t s);
 }  // namespace lgcn_detail
 
 namespace {
