@@ -57,11 +57,10 @@ def main():
                   f"[{os.environ.get('LGCN_LIB', 'product')} slots={os.environ.get('LGCN_EMU_SLOTS', '')}]"
                   f" all {' '.join(f'{t:.2f}' for t in ts)}", flush=True)
         return
-    for _, fn in runs:
-        for _ in range(3):
-            fn()
-    torch.cuda.synchronize()
     for name, fn in runs:
+        for _ in range(3):  # warm-up right before: the backward's schedule follows G's sparsity
+            fn()
+        torch.cuda.synchronize()
         time.sleep(0.05)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
