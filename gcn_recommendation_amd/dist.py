@@ -404,25 +404,60 @@ class ShardPropagate(torch.autograd.Function):
         return None, None, None, ctx.plan.backward(g.contiguous(), ctx.K, ctx.thr)
 
 
+class ShardPropagateSides(torch.autograd.Function):
+    """ShardPropagate on a side-major shard held as two blocks — slots [0, split) (users and
+    brands) and [split, n) (items) — as the model holds its user and item weights: the batch
+    gathers main.py makes (main.py:496-497) then index the block they read, so their gradients
+    are dense over that block only (a single [n x d] shard made every gather's IndexBackward
+    zero-fill and sum the whole table)."""
+
+    @staticmethod
+    def forward(ctx, plan, K, hub_thr, w0, w1):
+        ctx.plan, ctx.K, ctx.thr, ctx.split = plan, K, hub_thr, int(w0.shape[0])
+        out = engine.propagate_forward(plan.graph, [w0.detach(), w1.detach()], K, hub_thr)
+        return tuple(torch.split(out, [ctx.split, out.shape[0] - ctx.split], 0))
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        n = ctx.plan.graph.n_rows
+        d = next(g.shape[1] for g in (g0, g1) if g is not None)
+        gs = [g.contiguous() if g is not None else
+              torch.zeros((rows, d), dtype=torch.float32, device=ctx.plan.graph.device)
+              for g, rows in ((g0, ctx.split), (g1, n - ctx.split))]
+        g = engine.propagate_backward(ctx.plan.graph, gs, ctx.K, ctx.thr)
+        return None, None, None, g[:ctx.split], g[ctx.split:]
+
+
 def featsplit_train_timing(plan, x_slot, K, args, dev, hub_thr, batch=2048):
     """main.py's training step (main.py:488-531) on P ranks: every rank propagates its columns,
     gathers the batch rows of its shard, the sharded BPR loss reduces partial dots (one
     all_reduce), the backward runs on the shard's columns, Adam updates the shard. Identical
     batches on every rank (same seed). Edges/s = 2K·nnz / t, max over ranks."""
-    w = torch.nn.Parameter(x_slot.clone())
-    opt = torch.optim.Adam([w], lr=1e-3)
     U, I = args.users, args.items
     rng = np.random.default_rng(0)
     batches = [tuple(plan.slots(torch.from_numpy(a).to(dev)) for a in (
         rng.integers(0, U, batch), U + rng.integers(0, I, batch), U + rng.integers(0, I, batch)))
         for _ in range(args.train_steps + 2)]
     it = iter(batches)
+    sp_ = plan.graph.split
+    if sp_ is not None:  # side-major shard: two blocks, as the model's user / item weights
+        w0 = torch.nn.Parameter(x_slot[:sp_].clone())
+        w1 = torch.nn.Parameter(x_slot[sp_:].clone())
+        opt = torch.optim.Adam([w0, w1], lr=1e-3)
+    else:
+        w = torch.nn.Parameter(x_slot.clone())
+        opt = torch.optim.Adam([w], lr=1e-3)
 
     def step(timed):
         su, sp, sn = next(it)
         opt.zero_grad()
-        out = ShardPropagate.apply(plan, K, hub_thr, w)
-        loss = bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
+        if sp_ is not None:
+            o0, o1 = ShardPropagateSides.apply(plan, K, hub_thr, w0, w1)
+            sp1, sn1 = sp - sp_, sn - sp_
+            loss = bpr_loss_featsplit(o0[su], o1[sp1], o1[sn1], w0[su], w1[sp1], w1[sn1], 1e-4)
+        else:
+            out = ShardPropagate.apply(plan, K, hub_thr, w)
+            loss = bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4)
         loss.backward()
         opt.step()
         loss.item()  # main.py:527 reads the loss back every batch
@@ -430,7 +465,7 @@ def featsplit_train_timing(plan, x_slot, K, args, dev, hub_thr, batch=2048):
     ms, _ = _timed(step, args.train_steps, 2, dev)
     (ms_max,) = _max_over_ranks(torch.tensor([ms / args.train_steps], dtype=torch.float64,
                                              device=dev))
-    del w, opt
+    del opt
     return {"ms_per_step": round(ms_max, 3),
             "propagated_edges_per_s": round(2 * K * plan.graph.nnz / (ms_max / 1e3), 1),
             "batch": batch, "optimizer": "Adam(lr=1e-3) on the rank's shard",

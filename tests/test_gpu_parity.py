@@ -773,3 +773,63 @@ def test_featsplit_training_step_matches_single_gpu(gpu_device):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+def test_featsplit_sides_training_step_matches_single_gpu(gpu_device, monkeypatch):
+    """The N > 1 bench's training step on a side-major shard held as two blocks
+    (dist.ShardPropagateSides: users+brands / items, as the model's weights) == the drop-in
+    model's step: same loss, same gradients (1e-5), and == the one-block shard's gradients
+    bitwise."""
+    import socket
+    import torch.distributed as dist
+    from gcn_recommendation_amd import dist as D
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    own = not dist.is_initialized()
+    if own:
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+        s_.close()
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1)
+    try:
+        z = load_case("c1_nobrand")
+        U, I, B, d, K = case_dims(z)
+        n = U + I + B
+        m = _model(z, gpu_device)
+        adj = _adj(z, gpu_device)
+        bu, bp, bn = (torch.from_numpy(z[k]).to(gpu_device) for k in ("bpr_users", "bpr_pos",
+                                                                      "bpr_neg"))
+        fu, fi, fb, u0, i0 = m(adj, use_brand=False)
+        ref = bpr_loss_reg(fu[bu], fi[bp], fi[bn], u0[bu], i0[bp], i0[bn], 1e-4)
+        ref.backward()
+        r, c, v = z["adj_row"].astype(np.int64), z["adj_col"].astype(np.int64), z["adj_val"]
+        rowptr = np.searchsorted(r, np.arange(n + 1)).astype(np.int32)
+        plan = D.FeatSplitPlan(rowptr, c, v, n, gpu_device,
+                               sides=(U, U + I)).attach_transpose(rowptr, c, v)
+        sp_ = plan.graph.split
+        assert sp_ is not None
+        segs = [p.detach() for p in (m.user_embedding.weight, m.item_embedding.weight,
+                                     m.brand_embedding.weight)]
+        x, _ = plan.shard(segs, 1, 0)
+        thr = engine.hub_threshold_from_env()
+        su, sp, sn = plan.slots(bu), plan.slots(U + bp), plan.slots(U + bn)
+        w0 = torch.nn.Parameter(x[:sp_].clone())
+        w1 = torch.nn.Parameter(x[sp_:].clone())
+        o0, o1 = D.ShardPropagateSides.apply(plan, K, thr, w0, w1)
+        loss = D.bpr_loss_featsplit(o0[su], o1[sp - sp_], o1[sn - sp_], w0[su], w1[sp - sp_],
+                                    w1[sn - sp_], 1e-4)
+        loss.backward()
+        assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item())
+        w = torch.nn.Parameter(x.clone())   # the one-block shard
+        out = D.ShardPropagate.apply(plan, K, thr, w)
+        D.bpr_loss_featsplit(out[su], out[sp], out[sn], w[su], w[sp], w[sn], 1e-4).backward()
+        g2 = torch.cat([w0.grad, w1.grad]).cpu().numpy()
+        assert np.array_equal(g2, w.grad.cpu().numpy())
+        g = plan.unshard(torch.cat([w0.grad, w1.grad])).cpu().numpy()
+        assert_close_normwise(g[:U], m.user_embedding.weight.grad.cpu().numpy(), what="d user")
+        assert_close_normwise(g[U:U + I], m.item_embedding.weight.grad.cpu().numpy(),
+                              what="d item")
+    finally:
+        if own:
+            dist.destroy_process_group()
