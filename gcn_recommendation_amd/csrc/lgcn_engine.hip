@@ -489,11 +489,17 @@ const char* lgcn_error_string(int code) {
 }
 
 int32_t lgcn_chain_max_default(int64_t nnz) {
-    // a chain row must stay short against a whole layer (C3: 56M nonzeros, ~4 ms per layer ->
-    // 110k edges: forward 13.4 -> 13.2 ms and BPR backward 9.7 -> 9.4 ms against 55k; 220k:
-    // forward 12.8 ms but backward 10.2 ms); on a small graph the floor: a walk's fixed costs
-    // (block pass + walk ~0.4 ms per layer at C2) outweigh a 8k-edge chain (C2: 2048 -> 8192:
-    // forward 1.10 -> 0.94 ms)
+    // the forward's cut: a chain row must stay short against a whole layer; on a small graph the
+    // floor: a walk's fixed costs (block pass + walk ~0.4 ms per layer at C2) outweigh a 8k-edge
+    // chain (C2: 2048 -> 8192: forward 1.10 -> 0.94 ms). C3 (56M nonzeros): 55k / 110k / 220k /
+    // 330k edges: 13.4 / 13.06 / 12.65 / 12.8 ms (round 5, A/B on one box: 220k)
+    return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 256, 8192), 262144);
+}
+
+int32_t lgcn_chain_max_backward_default(int64_t nnz) {
+    // the backward's (Âᵀ) cut: its row-sparse first layer turns chain rows into live-edge chains
+    // and the longer rows into walks or live chains by their live edges; C3 BPR-batch backward
+    // 110k / 220k / 330k edges: 9.06 / 10.47 / 12.05 ms (round 5; 55k: 9.7 ms, round 4)
     return (int32_t)std::min<int64_t>(std::max<int64_t>(nnz / 512, 8192), 131072);
 }
 

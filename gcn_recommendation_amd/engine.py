@@ -88,14 +88,17 @@ def emu_min_degree_from_env(nnz=None):
     return int(load_library().lgcn_emu_min_default(int(nnz or 0)))
 
 
-def chain_max_degree(nnz):
+def chain_max_degree(nnz, backward=False):
     """Rows of the emulated-row list up to this degree run as sequential chains (lgcn_chain_rows,
     ~16 ns per edge), longer ones are block-emulated (block pass + walk): env LGCN_CHAIN_MAX, else
-    by graph size (lgcn_chain_max_default: a chain must stay short against the whole layer)."""
+    by graph size (lgcn_chain_max_default: a chain must stay short against the whole layer; the
+    backward's operator Âᵀ: lgcn_chain_max_backward_default)."""
     v = os.environ.get("LGCN_CHAIN_MAX", "")
     if v:
         return int(v)
-    return int(load_library().lgcn_chain_max_default(int(nnz)))
+    lib = load_library()
+    f = lib.lgcn_chain_max_backward_default if backward else lib.lgcn_chain_max_default
+    return int(f(int(nnz)))
 
 
 # Edges per hub chunk: LGCN_HUB_CHUNK, else by graph size (hub_chunk_for). A chunk is one lane
@@ -180,6 +183,7 @@ ABI = [
     ("lgcn_fusion_prelayer", ctypes.c_int, [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P,
                                             ctypes.c_float, _P, _I64, _P]),
     ("lgcn_chain_max_default", ctypes.c_int32, [_I64]),
+    ("lgcn_chain_max_backward_default", ctypes.c_int32, [_I64]),
     ("lgcn_plan_exact", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
     ("lgcn_emu_min_default", ctypes.c_int32, [_I64]),
     ("lgcn_plan_items", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
@@ -401,11 +405,11 @@ class HubPlan:
     def n_long(self):
         return self.n_items if self.mode == "exact" else 0
 
-    def walk_parts(self, nnz):
+    def walk_parts(self, nnz, backward=False):
         """(part_rows, part_blocks): the emulated rows cut into part 0 (rows of more than
         LGCN_EMU_PART0 = 8192 blocks, the longest walks: the layer's critical path), part 1 (more
         than chain_max_degree blocks) and the chain rows (lgcn_hub_plan_t emu_part_*)."""
-        b0, b1 = walk_cut_blocks(nnz)
+        b0, b1 = walk_cut_blocks(nnz, backward)
         nb = self.emu_nb
         cum = np.concatenate([[0], np.cumsum(nb)])
         r0, r1 = int((nb > b0).sum()), int((nb > b1).sum())
@@ -453,7 +457,8 @@ class HubPlan:
         if d is None:
             self._live = None
 
-    def struct(self, d, device, nnz=None, walk_all=False, scratch_set=0, live=False):
+    def struct(self, d, device, nnz=None, walk_all=False, scratch_set=0, live=False,
+               backward=False):
         """lgcn_hub_plan_t for width d. nnz: the operator's nonzeros (sets the chain/walk cut;
         None = every emulated row walked). walk_all: the chain rows are walked too (no chain
         kernel for this d / alignment, or LGCN_CHAIN=0), so the scratch covers every block.
@@ -463,7 +468,7 @@ class HubPlan:
             rows = [self.n_emu_rows, self.n_emu_rows] if nnz is None else None
             blocks = [self.n_emu_blocks, self.n_emu_blocks] if nnz is None else None
         if nnz is not None:
-            rows, blocks = self.walk_parts(nnz)
+            rows, blocks = self.walk_parts(nnz, backward)
         need = self.n_emu_blocks if (walk_all or nnz is None) else blocks[1]
         part, rel, meta, stage, eout = self.scratch(d, device, need, scratch_set)
         p = PlanT()
@@ -736,10 +741,10 @@ def classes_enabled():
     return os.environ.get("LGCN_CLASSES", "0") == "1"
 
 
-def walk_cut_blocks(nnz):
+def walk_cut_blocks(nnz, backward=False):
     """(b0, b1): the emulated rows of more than b0 blocks are part 0 (LGCN_EMU_PART0, 8192),
     of more than b1 = chain cut / LGCN_EMU_BLOCK part 1 (walked); the rest run as chains."""
-    b1 = -(-chain_max_degree(nnz) // LGCN_EMU_BLOCK)
+    b1 = -(-chain_max_degree(nnz, backward) // LGCN_EMU_BLOCK)
     return max(int(os.environ.get("LGCN_EMU_PART0", "8192")), b1), b1
 
 
@@ -1110,14 +1115,15 @@ emu_trace = None  # a list: spmm_layer appends (phase, torch.cuda.Event) of the 
 
 
 def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=None, x_div=1.0,
-               x_nz=None, kernel_events=None):
+               x_nz=None, kernel_events=None, backward=False):
     """One layer Y = epilogue(Â·(X / x_div)) under the operator's hub plan — lgcn_layer: the layer
     kernel (bundles, chunks, whole long rows) + chunk combine, the block pass + walk of the
     emulated parts and the chain rows, concurrently on the device's side streams (lgcn_sched,
     forked from and joined back into the caller's stream: graph-capture safe).
     x_nz: optional row bitmask of X (rows_nonzero; ADD epilogue only). kernel_events: optional
     (start, end) torch.cuda.Event pair recorded on the caller's stream around the layer kernel
-    (bench.py's live timing of that kernel)."""
+    (bench.py's live timing of that kernel). backward: the operator is the backward's Âᵀ (its
+    own chain cut, lgcn_chain_max_backward_default)."""
     lib = load_library()
     hp = hubs or graph.hubs(hub_threshold)
     stream = stream or _stream(graph.device)
@@ -1126,7 +1132,7 @@ def spmm_layer(graph, x_segments, y, d, epi, hub_threshold, hubs=None, stream=No
         raise LgcnError("spmm_layer: stream must be the device's current stream")
     chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and _aligned16(x_segments)
     plan = hp.struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
-                     live=x_nz is not None and live_enabled())
+                     live=x_nz is not None and live_enabled(), backward=backward)
     x = rows_desc(x_segments, d)
     sc = sched_for(graph.device) if hp.n_emu_rows else None
     args = (_ptr(graph.rowptr), _ptr(graph.edges), _ptr(graph.row_ids), graph.n_rows)
@@ -1167,7 +1173,8 @@ def live_enabled():
     return os.environ.get("LGCN_LIVE", "1") != "0"
 
 
-def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=False):
+def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=False,
+                backward=False):
     """The 8 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * segment + set] (segments: the
     side-0 classes, side 1). live: attach the live-edge scratch (the backward of a row-sparse
     G)."""
@@ -1178,7 +1185,8 @@ def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=Fal
     for g in range(N_SEGS):
         for j in (0, 1):
             arr[2 * g + j] = hps[g].struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
-                                           scratch_set=j, live=live and live_enabled())
+                                           scratch_set=j, live=live and live_enabled(),
+                                           backward=backward)
     return arr, hps
 
 
@@ -1418,7 +1426,7 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
         if use_sides(gt):
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
-                                   live=nz is not None)
+                                   live=nz is not None, backward=True)
             sc = sched_for(dev, role=_backward_role(dev, n, cnt))
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             sides = gt.sides_struct()
@@ -1440,7 +1448,8 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
         for k in range(1, K + 1):
             y = out if (K - k) % 2 == 0 else work
             spmm_layer(gt, h, y, d, ep, hub_threshold, hp, stream,
-                       x_div=float(K + 1) if k == 1 else 1.0, x_nz=nz if k == 1 else None)
+                       x_div=float(K + 1) if k == 1 else 1.0, x_nz=nz if k == 1 else None,
+                       backward=True)
             h = [y]
         return out
 

@@ -191,6 +191,9 @@ typedef struct {
  * emu_min_degree = the bundle threshold (128) for the default exact plan. Replaces, for a C
  * host, the Python planner engine.plan_hubs (which calls it). */
 int32_t lgcn_chain_max_default(int64_t nnz);
+/* the chain cut for the plans of the backward's operator Âᵀ (lgcn_propagate_backward*): the
+ * forward's default favours longer chains (fewer walks) than the backward's row-sparse layers do */
+int32_t lgcn_chain_max_backward_default(int64_t nnz);
 int lgcn_plan_exact(const int32_t* rowptr_host, const int32_t* row_ids_host, int32_t n_rows,
                     int32_t emu_min_degree, int32_t chain_max, int32_t part0_blocks,
                     lgcn_emu_row_t* rows_host, lgcn_emu_block_t* blocks_host,

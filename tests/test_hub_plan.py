@@ -152,9 +152,14 @@ def test_c_planner_parts_and_scratch():
                                rows.ctypes.data, blocks.ctypes.data, ctypes.byref(plan)) == 0
     assert list(rows[:, 2]) == nb
     hp = engine.HubPlan(128, emu_nb=np.array(nb))
-    pr, pb = hp.walk_parts(60_000 * 512)  # chain_max_degree(nnz) = 60_000
+    pr, pb = hp.walk_parts(60_000 * 256)  # chain_max_degree(nnz) = 60_000 (the forward's)
     assert pr[0] == plan.emu_part_rows[0]
-    assert hp.struct(64, "cpu", nnz=60_000 * 512).emu_part_max_blocks[0] == \
+    assert list(pr) == list(plan.emu_part_rows) and list(pb) == list(plan.emu_part_blocks)
+    # the backward's operator: its own default, nnz / 512
+    assert lib.lgcn_chain_max_default(60_000 * 256) == 60_000
+    assert lib.lgcn_chain_max_backward_default(60_000 * 512) == 60_000
+    assert list(hp.walk_parts(60_000 * 512, backward=True)[0]) == list(plan.emu_part_rows)
+    assert hp.struct(64, "cpu", nnz=60_000 * 256).emu_part_max_blocks[0] == \
         plan.emu_part_max_blocks[0]
     sizes = (ctypes.c_size_t * 3)()
     assert lib.lgcn_plan_scratch_bytes(ctypes.byref(plan), 64, 0, sizes) == 0
@@ -169,5 +174,8 @@ def test_c_planner_parts_and_scratch():
     assert lib.lgcn_plan_exact(rowptr.ctypes.data, None, deg.size, 128, 0, 0, rows.ctypes.data,
                                None, ctypes.byref(plan)) == -1
     assert lib.lgcn_chain_max_default(1_600_000) == 8192
-    assert lib.lgcn_chain_max_default(56_300_000) == 56_300_000 // 512
-    assert lib.lgcn_chain_max_default(10 ** 10) == 131072
+    assert lib.lgcn_chain_max_default(56_300_000) == 56_300_000 // 256
+    assert lib.lgcn_chain_max_default(10 ** 10) == 262144
+    assert lib.lgcn_chain_max_backward_default(1_600_000) == 8192
+    assert lib.lgcn_chain_max_backward_default(56_300_000) == 56_300_000 // 512
+    assert lib.lgcn_chain_max_backward_default(10 ** 10) == 131072
