@@ -1291,7 +1291,8 @@ bool capturing(hipStream_t s) {
 // The two lanes: lane 1 on its own streams when the schedule has them, else both lanes share
 // the caller's stream (half-layers then run in layer order, each still overlapped inside).
 // While `s` is being captured, lane 1 runs its half-layers on its main stream alone: a capture
-// that forks lane 1's own aux streams crashes hipStreamEndCapture on this ROCm (rounds 3-5,
+// that forks lane 1's own aux streams crashes hipStreamEndCapture on ROCm 7.2.0 with PyTorch
+// 2.10.0+rocm7.0 (this image's HIP runtime; rounds 3-5,
 // with every record on its own event too, while a plain-HIP replay of the same
 // stream/event sequence captures fine). The diagnostic build LGCN_CAPTURE_AUX_EXP keeps them.
 #ifdef LGCN_CAPTURE_AUX_EXP
