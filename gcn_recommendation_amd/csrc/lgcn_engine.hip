@@ -440,6 +440,31 @@ int valid_geom(int32_t n_rows, int32_t d) {
 // =============================================================================================
 // C ABI
 // =============================================================================================
+// dst += src where src != 0, elementwise (lgcn_add_nonzero): src is a row-sparse gradient (the
+// rows main.py gathers), dst a dense one that is never -0 (every engine output row is a chain from
+// +0 or a sum with one: DESIGN §4d), so dst + (+-0) == dst and skipping the zeros gives the dense
+// add's bits while reading dst only where src holds a value. NaN != 0: added.
+template <typename V>
+__global__ __launch_bounds__(256) void k_add_nonzero(const V* __restrict__ src, V* __restrict__ dst,
+                                                     int64_t m) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m;
+         i += (int64_t)gridDim.x * 256) {
+        const V v = src[i];
+        if constexpr (sizeof(V) == 16) {
+            if (v.x != 0.f || v.y != 0.f || v.z != 0.f || v.w != 0.f) {
+                V a = dst[i];
+                a.x = a.x + v.x;
+                a.y = a.y + v.y;
+                a.z = a.z + v.z;
+                a.w = a.w + v.w;
+                dst[i] = a;
+            }
+        } else if (v != 0.f) {
+            dst[i] = dst[i] + v;
+        }
+    }
+}
+
 extern "C" {
 
 int lgcn_abi_version(void) { return LGCN_ABI_VERSION; }
@@ -925,6 +950,24 @@ int lgcn_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t d, uint32_t* mask, 
     const Geo g = pick_geo(d, rows_aligned(x));
     NonzeroF f{&x, n_rows, g.dW, mask, count, s};
     return dispatch_geo(g, f);
+}
+
+int lgcn_add_nonzero(const float* src, float* dst, int64_t n, void* stream) {
+    if (n < 0) return LGCN_EINVAL;
+    if (n == 0) return 0;
+    if (!src || !dst) return LGCN_EINVAL;
+    hipStream_t s = S(stream);
+    const bool vec = n % 4 == 0 && !(reinterpret_cast<uintptr_t>(src) & 15) &&
+                     !(reinterpret_cast<uintptr_t>(dst) & 15);
+    const int64_t m = vec ? n / 4 : n;
+    const int64_t grid = std::min<int64_t>((m + 255) / 256, 1 << 20);
+    if (vec)
+        hipLaunchKernelGGL((k_add_nonzero<float4>), dim3((uint32_t)grid), dim3(256), 0, s,
+                           reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst), m);
+    else
+        hipLaunchKernelGGL((k_add_nonzero<float>), dim3((uint32_t)grid), dim3(256), 0, s, src,
+                           dst, m);
+    return herr(hipGetLastError());
 }
 
 int lgcn_hub_combine(const lgcn_hub_row_t* hub_rows, int32_t n_hub_rows, int32_t n_pre_rows,

@@ -194,6 +194,7 @@ ABI = [
     ("lgcn_spmm_layer", ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _I32, _P, RowsT, ctypes.c_float,
                                        _P, _P, _I64, _I32, ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_rows_nonzero", ctypes.c_int, [RowsT, _I32, _I32, _P, _P, _P]),
+    ("lgcn_add_nonzero", ctypes.c_int, [_P, _P, _I64, _P]),
     ("lgcn_hub_combine", ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _I32,
                                         ctypes.POINTER(EpilogueT), _P]),
     ("lgcn_scale_rows", ctypes.c_int, [RowsT, _I32, _I32, ctypes.c_float, _P, _I64, _P]),
@@ -1483,26 +1484,51 @@ class CapturedForward:
 class PropagateFunction(torch.autograd.Function):
     """(user, item, brand) weights -> the (user, item, brand) blocks of the mean of K propagated
     layers (views of one buffer: no torch.cat / torch.split copies either way); backward by the
-    same kernel, reading the three output gradients in place."""
+    same kernel, reading the three output gradients in place.
+
+    n_e0 > 0 also returns the first n_e0 weights themselves (storage-sharing aliases, not views:
+    an optimizer's in-place update shows through them) as further outputs — the ego tables the
+    model hands back (lightgcn.py:81) for main.py's regulariser gather (main.py:497). Their
+    gradients then reach this backward instead of the weights, and it adds them into the engine's
+    dE0 blocks at their nonzero entries only (lgcn_add_nonzero): the sum autograd would form, to
+    the bit (dE0 is never -0), without its dense read-read-write of the whole table."""
 
     @staticmethod
-    def forward(ctx, graph, K, hub_threshold, *segments):
+    def forward(ctx, graph, K, hub_threshold, n_e0, *segments):
         ctx.graph, ctx.K, ctx.hub_threshold = graph, K, hub_threshold
         ctx.sizes = [int(t.shape[0]) for t in segments]
         segs = [t.detach() for t in segments]
         out = propagate_forward(graph, segs, K, hub_threshold)
-        return tuple(torch.split(out, ctx.sizes, 0))
+        return tuple(torch.split(out, ctx.sizes, 0)) + tuple(segs[:n_e0])
 
     @staticmethod
     def backward(ctx, *grads):
+        nseg = len(ctx.sizes)
+        head = (None, None, None, None)
+        gout, ge0 = grads[:nseg], grads[nseg:]
         d = next((g.shape[1] for g in grads if g is not None), None)
         if d is None:
-            return (None, None, None) + (None,) * len(grads)
+            return head + (None,) * nseg
+        if all(g is None for g in gout):  # only the ego aliases were used
+            return head + tuple(ge0) + (None,) * (nseg - len(ge0))
         gs = [g if g is not None else
               torch.zeros((sz, d), dtype=torch.float32, device=ctx.graph.device)
-              for g, sz in zip(grads, ctx.sizes)]
+              for g, sz in zip(gout, ctx.sizes)]
         g0 = propagate_backward(ctx.graph, gs, ctx.K, ctx.hub_threshold)
-        return (None, None, None) + tuple(torch.split(g0, ctx.sizes, 0))
+        blocks = torch.split(g0, ctx.sizes, 0)
+        lib = load_library()
+        dev = ctx.graph.device
+        for g, blk in zip(ge0, blocks):
+            if g is None:
+                continue
+            g = g.contiguous()
+            if g.dtype != torch.float32 or g.shape != blk.shape or g.device != blk.device:
+                raise LgcnError(f"ego gradient {tuple(g.shape)} {g.dtype} does not match its "
+                                f"block {tuple(blk.shape)}")
+            with torch.cuda.device(dev):
+                _check(lib.lgcn_add_nonzero(_ptr(g), _ptr(blk), g.numel(), _stream(dev)),
+                       "lgcn_add_nonzero")
+        return head + tuple(blocks)
 
 
 def segment_sides(segments):
@@ -1514,14 +1540,17 @@ def segment_sides(segments):
     return (lo, lo + int(segments[1].shape[0]))
 
 
-def propagate_blocks(adj, segments, K, hub_threshold=None):
+def propagate_blocks(adj, segments, K, hub_threshold=None, e0_outputs=0):
     """Autograd-aware engine entry used by models.LightGCN / LightGCN_Fusion on a HIP device:
     returns the final embeddings as one block per input segment (user, item, brand). The item
-    rows are offered as the bipartite sides (graph_from_coo)."""
+    rows are offered as the bipartite sides (graph_from_coo). e0_outputs = n appends aliases of
+    the first n segments whose gradients the backward folds into its own (PropagateFunction)."""
     graph = graph_from_coo(adj, sides=segment_sides(segments))
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
-    return PropagateFunction.apply(graph, K, hub_threshold, *segments)
+    if not 0 <= e0_outputs <= len(segments):
+        raise LgcnError(f"e0_outputs={e0_outputs} for {len(segments)} segments")
+    return PropagateFunction.apply(graph, K, hub_threshold, e0_outputs, *segments)
 
 
 def propagate(adj, segments, K, hub_threshold=None):

@@ -391,6 +391,11 @@ int lgcn_rows_nonzero(lgcn_rows_t x, int32_t n_rows, int32_t d, uint32_t* mask, 
                       void* stream);
 
 /* Y[r,:] = X[r,:] / div for r < n_rows (mean of one layer; backward seed G/(K+1)). */
+/* dst[i] = dst[i] + src[i] wherever src[i] != 0 (n floats each): the gradient of layer-0 rows a
+ * training step gathers (main.py:497, a row-sparse [rows x d] block) accumulated into the
+ * propagation's dense gradient — the autograd accumulation of the two, reading dst only where src
+ * holds a value (bitwise the dense add: dst is never -0). */
+int lgcn_add_nonzero(const float* src, float* dst, int64_t n, void* stream);
 int lgcn_scale_rows(lgcn_rows_t x, int32_t n_rows, int32_t d, float div, float* y, int64_t ldy,
                     void* stream);
 

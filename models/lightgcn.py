@@ -46,9 +46,11 @@ class LightGCN(nn.Module):
 
     # -- propagation ------------------------------------------------------------------------
     def _propagate(self, adj_mat, segments):
-        """(final_user, final_item, final_brand) blocks."""
+        """(final_user, final_item, final_brand) blocks, then the user and item ego tables: on a
+        HIP device the engine's aliases of them (their gradients join the propagation's inside
+        its backward — engine.PropagateFunction), on a CPU adjacency the weights themselves."""
         if adj_mat.device.type == "cuda":
-            final = engine.propagate_blocks(adj_mat, segments, self.n_layers)
+            final = engine.propagate_blocks(adj_mat, segments, self.n_layers, e0_outputs=2)
             if self.debug and self.n_layers > 0:  # lightgcn.py:44-51 prints once per layer
                 with torch.no_grad():
                     _, layers = engine.propagate_forward(
@@ -71,7 +73,8 @@ class LightGCN(nn.Module):
                 brand_emb_i = ego[self.num_users + self.num_items:]
                 print(f"Layer {i + 1} brand embedding L2 norm: {brand_emb_i.norm(2).item():.6f}")
         final = torch.mean(torch.stack(all_embeddings, dim=0), dim=0)
-        return torch.split(final, [self.num_users, self.num_items, self.num_brands])
+        return torch.split(final, [self.num_users, self.num_items, self.num_brands]) + \
+            (segments[0], segments[1])
 
     def _last_layer(self, adj_mat, layers, segments):
         g = engine.graph_from_coo(adj_mat, engine.segment_sides(segments))
@@ -85,8 +88,8 @@ class LightGCN(nn.Module):
         user_emb_0 = self.user_embedding.weight
         item_emb_0 = self.item_embedding.weight
         brand_emb_0 = self.brand_embedding.weight
-        final_user_emb, final_item_emb, final_brand_emb = self._propagate(
-            adj_mat, [user_emb_0, item_emb_0, brand_emb_0])
+        final_user_emb, final_item_emb, final_brand_emb, user_emb_0, item_emb_0 = \
+            self._propagate(adj_mat, [user_emb_0, item_emb_0, brand_emb_0])
         if self.debug:
             self._debug_cosine(adj_mat, final_item_emb, user_emb_0, item_emb_0)
         return final_user_emb, final_item_emb, final_brand_emb, user_emb_0, item_emb_0

@@ -48,8 +48,10 @@ class LightGCN_Fusion(nn.Module):
         fused_item_emb_0 = self.fused_item_embedding()
         segments = [user_emb_0, fused_item_emb_0, brand_emb_0]
         if adj_mat.device.type == "cuda":
-            final_user_emb, final_item_emb, final_brand_emb = engine.propagate_blocks(
-                adj_mat, segments, self.n_layers)
+            # user_emb_0 as the engine's alias: its gradient joins the propagation's inside the
+            # backward (engine.PropagateFunction, e0_outputs)
+            final_user_emb, final_item_emb, final_brand_emb, user_emb_0 = engine.propagate_blocks(
+                adj_mat, segments, self.n_layers, e0_outputs=1)
         else:  # CPU adjacency: the reference's ATen path (lightgcn_fusion.py:52-59)
             ego = torch.cat(segments, dim=0)
             all_embeddings = [ego]

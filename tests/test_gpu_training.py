@@ -46,3 +46,57 @@ def test_training_loop_gpu_matches_cpu(gpu_device):
     for k in pc:
         np.testing.assert_allclose(pg[k], pc[k], rtol=0, atol=2e-6 * np.abs(pc[k]).max() + 1e-9)
         assert not np.array_equal(pc[k], z0[k]) or pc[k].size == 0, f"{k} never updated"
+
+
+def _ego_grads(dev, z, e0_outputs, dense=False):
+    """Weight gradients of one BPR step (main.py:496-499) whose regulariser gathers either the
+    engine's ego aliases (e0_outputs=2) or the weights themselves (0)."""
+    from gcn_recommendation_amd import engine
+    U, I, B, d, K = case_dims(z)
+    torch.manual_seed(7)
+    w = [torch.randn(n, d, device=dev).requires_grad_() for n in (U, I, B)]
+    adj = graph.build_norm_adj(z["train_user"], z["train_item"], U, I, B, z["ib_item"],
+                               z["ib_brand"], bool(z["use_brand"]), device=dev)
+    out = engine.propagate_blocks(adj, w, K, e0_outputs=e0_outputs)
+    fu, fi, fb = out[:3]
+    u0, i0 = out[3:] if e0_outputs else (w[0], w[1])
+    g = torch.Generator().manual_seed(11)
+    bu, bp, bn = (torch.randint(0, n, (512,), generator=g).to(dev) for n in (U, I, I))
+    loss = bpr_loss_reg(fu[bu], fi[bp], fi[bn], u0[bu], i0[bp], i0[bn], 1e-4, final_brand_emb=fb)
+    if dense:  # every row of every table live: the dense add
+        loss = loss + (fu * 1e-3).sum() + (u0 * 2e-3).sum() + (i0 ** 2).sum()
+    loss.backward()
+    return [t.grad.clone() for t in w]
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_ego_alias_gradients_bitwise(gpu_device, dense):
+    """PropagateFunction's ego aliases: adding their gradients' nonzero entries into dE0 inside
+    the backward gives autograd's dense sum to the bit (row-sparse and dense cases)."""
+    z = load_case("c1_brand")
+    a = _ego_grads(gpu_device, z, 2, dense)
+    b = _ego_grads(gpu_device, z, 0, dense)
+    for x, y in zip(a, b):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
+def test_add_nonzero_matches_dense_add(gpu_device):
+    """lgcn_add_nonzero == dst + src bitwise for dst != -0 (zeros of both signs, NaN, inf, odd
+    lengths and a misaligned start take the scalar path)."""
+    from gcn_recommendation_amd import engine
+    lib = engine.load_library()
+    g = torch.Generator().manual_seed(3)
+    for n, off in ((0, 0), (1, 0), (7, 0), (4096, 0), (4096 + 3, 1), (1 << 20, 0)):
+        src = torch.randn(n + off, generator=g)
+        src[torch.rand(n + off, generator=g) < 0.6] = 0.0
+        src[torch.rand(n + off, generator=g) < 0.1] = -0.0
+        if n > 8:
+            src[off + 3], src[off + 5] = float("nan"), float("inf")
+        dst = torch.randn(n + off, generator=g)
+        dst[torch.rand(n + off, generator=g) < 0.2] = 0.0
+        s, t = src.to(gpu_device)[off:], dst.to(gpu_device)[off:]
+        want = t + s
+        with torch.cuda.device(gpu_device):
+            assert lib.lgcn_add_nonzero(engine._ptr(s), engine._ptr(t), n,
+                                        engine._stream(gpu_device)) == 0
+        assert torch.equal(t.view(torch.int32), want.view(torch.int32)), n
