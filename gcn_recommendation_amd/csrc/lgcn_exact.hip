@@ -417,14 +417,7 @@ __device__ __forceinline__ uint32_t lds_byte(const void* p) {
 // Inline asm on purpose: a compiler-visible LDS-DMA makes the compiler drain every global load
 // in flight (vmcnt(0)) before any later LDS access of the kernel, which would serialise the
 // walker's prefetches; hidden from it, the DMA is waited for by this file's explicit vmcnt.
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
-}
-
-// Two 1-KB LDS-DMAs to consecutive KB of LDS (dst, dst + 1024): one m0 save/restore.
+// dma16x2: two of them to consecutive KB of LDS (dst, dst + 1024) under one m0 save/restore.
 __device__ __forceinline__ void dma16x2(const void* g0, const void* g1, uint32_t dst) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
@@ -433,6 +426,35 @@ __device__ __forceinline__ void dma16x2(const void* g0, const void* g1, uint32_t
                  : "=&s"(keep) : "v"(g0), "v"(g1),
                    "s"(__builtin_amdgcn_readfirstlane((int)dst)) : "memory", "scc");
 }
+
+// N (4 or 8) 1-KB LDS-DMAs to consecutive KB of LDS (dst + 1024 k): a chain window's gathers
+// under one m0 save/restore (k_chain_rows; 3 scalar instructions per load saved).
+#define LGCN_DMA16_NEXT(i) \
+    "global_load_lds_dwordx4 %" #i ", off\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+template <int N>
+__device__ __forceinline__ void dma16_run(const char* const (&g)[N], uint32_t dst) {
+    static_assert(N == 2 || N == 4 || N == 8, "window sizes of k_chain_rows");
+    uint32_t keep;
+    if constexpr (N == 2) {
+        dma16x2(g[0], g[1], dst);
+    } else if constexpr (N == 4) {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
+                     LGCN_DMA16_NEXT(1) LGCN_DMA16_NEXT(2) LGCN_DMA16_NEXT(3)
+                     "global_load_lds_dwordx4 %4, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "s"(dst)
+                     : "memory", "scc");
+    } else {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %9\n\ts_nop 0\n\t"
+                     LGCN_DMA16_NEXT(1) LGCN_DMA16_NEXT(2) LGCN_DMA16_NEXT(3)
+                     LGCN_DMA16_NEXT(4) LGCN_DMA16_NEXT(5) LGCN_DMA16_NEXT(6)
+                     LGCN_DMA16_NEXT(7)
+                     "global_load_lds_dwordx4 %8, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]),
+                       "v"(g[5]), "v"(g[6]), "v"(g[7]), "s"(dst)
+                     : "memory", "scc");
+    }
+}
+#undef LGCN_DMA16_NEXT
 
 // s_waitcnt vmcnt(m) for the largest m in {32, 16, 8, 4, 2, 1, 0} not above a wave-uniform n:
 // at most n younger operations may stay outstanding, a few of them may be waited for too. The
@@ -1009,13 +1031,15 @@ struct ChainCfg {
     static constexpr int NR = W == 32 && AHEAD <= 7 ? 16 : 2 * AHEAD + 1;
 };
 
-// 4 bytes per lane by LDS-DMA: lane l's dword at gsrc -> LDS byte address dst + 4 l (dst
-// wave-uniform); hidden from the compiler like dma16.
-__device__ __forceinline__ void dma4(const void* gsrc, uint32_t dst) {
+// the two dword LDS-DMAs of a window's edge records (column -> dst0, value -> dst1; lane l's
+// dword to dst + 4 l), one m0 save/restore; hidden from the compiler like dma16x2
+__device__ __forceinline__ void dma4x2(const void* g0, uint32_t dst0, const void* g1,
+                                       uint32_t dst1) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g0), "v"(g1), "s"(dst0), "s"(dst1) : "memory");
 }
 
 template <int N>
@@ -1051,8 +1075,8 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     const int32_t* ew = reinterpret_cast<const int32_t*>(edges);
     auto rec_dma = [&](int32_t w) {
         const int64_t j = min((int64_t)beg + 64 * w + lane, (int64_t)end - 1);
-        dma4(ew + 2 * j, lds_byte(&s_col[w % NR][0]));
-        dma4(ew + 2 * j + 1, lds_byte(&s_val[w % NR][0]));
+        dma4x2(ew + 2 * j, lds_byte(&s_col[w % NR][0]), ew + 2 * j + 1,
+               lds_byte(&s_val[w % NR][0]));
     };
     // gathered X of window w -> s_x[w % NX]: instruction k moves rows k*RPI .. k*RPI + RPI - 1
     // (lane -> row sub = lane / LPR, 16-B piece q = lane % LPR); the columns come from LDS
@@ -1064,13 +1088,15 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
 #pragma unroll
         for (int k = 0; k < C::NI; ++k) cols[k] = s_col[w % NR][k * C::RPI + sub];
         const uint32_t dst = lds_byte(s_x[w % NX]);
+        const char* g[C::NI];
 #pragma unroll
         for (int k = 0; k < C::NI; ++k) {
             if constexpr (SEG1)  // one buffer: a row is base + col * ld
-                dma16(xb + (uint64_t)(uint32_t)cols[k] * row_b, dst + k * 1024);
+                g[k] = xb + (uint64_t)(uint32_t)cols[k] * row_b;
             else
-                dma16(seg_row_sel(x, cols[k]) + c0 + 4 * q, dst + k * 1024);
+                g[k] = reinterpret_cast<const char*>(seg_row_sel(x, cols[k]) + c0 + 4 * q);
         }
+        dma16_run<C::NI>(g, dst);  // instruction k -> dst + 1024 k
     };
     // Pipeline (A = AHEAD): iteration v issues x(v + A) then rec(v + 2A); the prologue runs
     // v = -A .. -1 after rec(0 .. A-1) have landed. At iteration w, x(w) and rec(w + A) (both
