@@ -1,0 +1,9 @@
+# Round-end C3 evidence in one call: rocprofv3 trace + PMC passes, the stamped traffic file,
+# then the default bench line that reads it. Outputs under gpurun_out/final/.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/final
+bash tools/profile.sh c3 --steps 10 --no-cpu-baseline --train-steps 0 --recall-epochs 0 --no-c4 || exit 1
+python tools/summarize_profile.py gpurun_out/prof_c3 c3_powerlaw r05 6828419628 > gpurun_out/final/summary.txt 2>&1 || exit 1
+cp profiles/traffic_c3_powerlaw.json profiles/r05_c3_powerlaw_kernel_stats.csv gpurun_out/final/
+timeout -k 10 900 python -u bench.py > gpurun_out/final/bench_c3.log 2>&1 || exit 1
