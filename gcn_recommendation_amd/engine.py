@@ -1545,11 +1545,11 @@ def propagate_blocks(adj, segments, K, hub_threshold=None, e0_outputs=0):
     returns the final embeddings as one block per input segment (user, item, brand). The item
     rows are offered as the bipartite sides (graph_from_coo). e0_outputs = n appends aliases of
     the first n segments whose gradients the backward folds into its own (PropagateFunction)."""
+    if not 0 <= e0_outputs <= len(segments):
+        raise LgcnError(f"e0_outputs={e0_outputs} for {len(segments)} segments")
     graph = graph_from_coo(adj, sides=segment_sides(segments))
     if hub_threshold is None:
         hub_threshold = hub_threshold_from_env()
-    if not 0 <= e0_outputs <= len(segments):
-        raise LgcnError(f"e0_outputs={e0_outputs} for {len(segments)} segments")
     return PropagateFunction.apply(graph, K, hub_threshold, e0_outputs, *segments)
 
 

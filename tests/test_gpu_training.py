@@ -100,3 +100,36 @@ def test_add_nonzero_matches_dense_add(gpu_device):
             assert lib.lgcn_add_nonzero(engine._ptr(s), engine._ptr(t), n,
                                         engine._stream(gpu_device)) == 0
         assert torch.equal(t.view(torch.int32), want.view(torch.int32)), n
+
+
+def test_fusion_model_user_alias_gradients_bitwise(gpu_device):
+    """LightGCN_Fusion returns the engine's user alias (e0_outputs=1): one BPR step's parameter
+    gradients equal those of the same step with the user weight itself, to the bit."""
+    from models.lightgcn_fusion import LightGCN_Fusion
+    from gcn_recommendation_amd import engine
+    z = load_case("c1_fusion")
+    U, I, B, d, K = case_dims(z)
+    content = z["content"] if "content" in z.files else \
+        np.random.default_rng(1).standard_normal((I, 32)).astype(np.float32)
+    adj = graph.build_norm_adj(z["train_user"], z["train_item"], U, I, B, z["ib_item"],
+                               z["ib_brand"], bool(z["use_brand"]), device=gpu_device)
+    g = torch.Generator().manual_seed(5)
+    bu, bp, bn = (torch.randint(0, n, (256,), generator=g).to(gpu_device) for n in (U, I, I))
+
+    def grads(alias):
+        torch.manual_seed(3)
+        m = LightGCN_Fusion(U, I, B, Cfg(d, K), pretrained_item_emb=content).to(gpu_device)
+        fu, fi, fb, u0, i0 = m(adj)
+        if not alias:
+            u0 = m.user_embedding.weight
+        else:
+            assert u0 is not m.user_embedding.weight
+            assert u0.data_ptr() == m.user_embedding.weight.data_ptr()
+        loss = bpr_loss_reg(fu[bu], fi[bp], fi[bn], u0[bu], i0[bp], i0[bn], 1e-4,
+                            final_brand_emb=fb)
+        loss.backward()
+        return {k: p.grad.clone() for k, p in m.named_parameters()}
+
+    a, b = grads(True), grads(False)
+    for k in a:
+        assert torch.equal(a[k].view(torch.int32), b[k].view(torch.int32)), k

@@ -121,3 +121,22 @@ def test_use_brand_flag_is_ignored_like_reference():
     a = m(adj, use_brand=True)[0]
     b = m(adj, use_brand=False)[0]
     assert torch.equal(a, b)
+
+
+def test_cpu_forward_returns_the_weights_themselves():
+    """On a CPU adjacency the ego tables are the weights (the reference's objects); the engine's
+    aliases (e0_outputs) exist on the HIP path only. A bad e0_outputs is refused before any
+    device work."""
+    from gcn_recommendation_amd import engine
+    from models.lightgcn import LightGCN
+    z = load_case("c1_brand")
+    U, I, B, d, K = case_dims(z)
+    m = LightGCN(U, I, B, Cfg(d, K))
+    adj = graph.build_norm_adj(z["train_user"], z["train_item"], U, I, B, z["ib_item"],
+                               z["ib_brand"], bool(z["use_brand"]))
+    out = m(adj)
+    assert out[3] is m.user_embedding.weight and out[4] is m.item_embedding.weight
+    segs = [torch.zeros(2, 4)] * 3
+    for bad in (-1, 4):
+        with pytest.raises(engine.LgcnError):
+            engine.propagate_blocks(adj, segs, 1, e0_outputs=bad)
