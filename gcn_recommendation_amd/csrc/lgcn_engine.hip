@@ -238,6 +238,28 @@ __global__ void k_class_mark(const int32_t* __restrict__ rowptr,
         atomicMin(mark + load_edge(edges + j).x, part);
 }
 
+// partof[row_ids[s_lo + i]] = part of side-1 slot s_lo + i (0 below s_mid, 1 above)
+__global__ void k_class_partof(const int32_t* __restrict__ row_ids, int32_t s_lo, int32_t s_mid,
+                               int32_t s_hi, int32_t* __restrict__ partof) {
+    const int64_t s = s_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= s_hi) return;
+    partof[row_ids[s]] = s < s_mid ? 0 : 1;
+}
+
+// the other direction (Â need not be structurally symmetric): side-0 slot s reads a walked
+// side-1 row -> mark[row_ids[s]] = min(mark, that row's part); one thread per side-0 slot
+__global__ void k_class_mark_rev(const int32_t* __restrict__ rowptr,
+                                 const lgcn_edge_t* __restrict__ edges,
+                                 const int32_t* __restrict__ row_ids, int32_t n0,
+                                 const int32_t* __restrict__ partof, int32_t* __restrict__ mark) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n0) return;
+    int m = 2;
+    for (int64_t j = rowptr[s], end = rowptr[s + 1]; j < end && m > 0; ++j)
+        m = min(m, partof[load_edge(edges + j).x]);
+    if (m < 2) atomicMin(mark + row_ids[s], m);
+}
+
 __global__ void k_class_keys(const int32_t* __restrict__ row_ids, const int32_t* __restrict__ mark,
                              int32_t n0, int32_t* __restrict__ key, int32_t* __restrict__ iota) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -639,6 +661,27 @@ int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host) {
     return 0;
 }
 
+int lgcn_stream_create_dedicated(void** stream) {
+    if (!stream) return LGCN_EINVAL;
+    int dev = 0, n_cu = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return (int)e;
+    if (hipError_t e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev))
+        return (int)e;
+    if (n_cu < 1 || n_cu > 1024) return LGCN_EINVAL;
+    uint32_t mask[32];
+    const int words = (n_cu + 31) / 32;
+    for (int i = 0; i < words; ++i) mask[i] = 0xffffffffu;
+    if (n_cu % 32) mask[words - 1] = (1u << (n_cu % 32)) - 1u;
+    hipStream_t s = nullptr;
+    if (hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask)) return (int)e;
+    *stream = s;
+    return 0;
+}
+
+int lgcn_stream_destroy(void* stream) {
+    return stream ? herr(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream))) : 0;
+}
+
 int lgcn_coo_inspect(const int64_t* rows, const int64_t* cols, int64_t nnz, int32_t n_rows,
                      int32_t n_cols, int32_t* flags, void* stream) {
     if (nnz < 0 || !flags) return LGCN_EINVAL;
@@ -831,6 +874,19 @@ int lgcn_csr_side_classes(const int32_t* rowptr, const lgcn_edge_t* edges, const
         hipLaunchKernelGGL(k_class_mark, dim3((uint32_t)part_rows1, 256), dim3(kBlock), 0, s, rowptr,
                            edges, split, split + part_rows0, mark);
         if (int e = last_err()) return e;
+        if (n0 > 0) {
+            // the side-0 rows that read a walked row (not implied without structural
+            // symmetry); key_sorted holds partof[row id] until the sort below rewrites it
+            int32_t* partof = key_sorted;
+            hipLaunchKernelGGL(k_fill_i32, grid(n), dim3(kBlock), 0, s, partof, (int64_t)n, 2);
+            if (int e = last_err()) return e;
+            hipLaunchKernelGGL(k_class_partof, grid(part_rows1), dim3(kBlock), 0, s, row_ids,
+                               split, split + part_rows0, split + part_rows1, partof);
+            if (int e = last_err()) return e;
+            hipLaunchKernelGGL(k_class_mark_rev, grid(n0), dim3(kBlock), 0, s, rowptr, edges,
+                               row_ids, n0, partof, mark);
+            if (int e = last_err()) return e;
+        }
     }
     if (n0 > 0) {
         hipLaunchKernelGGL(k_class_keys, grid(n0), dim3(kBlock), 0, s, row_ids, mark, n0, key, iota);
@@ -999,8 +1055,8 @@ namespace {
 // Every event record of one call takes a fresh event from this pool, so no event is recorded
 // twice inside one call (a captured graph's edges follow the records one to one); the next call
 // starts over. Created by lgcn_sched_create — nothing is created while a stream is captured. A
-// call that needs more wraps around (eager runs stay ordered: a wait binds to the record before
-// it).
+// call that would need more fails with LGCN_ETOOMANY instead of reusing an event (a reused event
+// could bind a cross-layer wait to a later record; ~30 records per layer, K <= 17, use < 600).
 constexpr int kPoolEvents = 1024;
 struct EventPool {
     hipEvent_t ev[kPoolEvents];
@@ -1025,6 +1081,7 @@ struct lgcn_sched {
     hipEvent_t* trace_sides;   // optional [32 K] (LGCN_SCHED_TRACE_SIDES)
     hipEvent_t* timing_sides;  // optional [8 K] (LGCN_SCHED_TIMING_SIDES)
     int classes;               // LGCN_SCHED_CLASSES (default 1)
+    int lk_normal;             // LGCN_SCHED_LK_NORMAL (default 1)
 };
 
 namespace {
@@ -1035,7 +1092,7 @@ struct EmuPart {
 int ev_next(const lgcn_sched* sc, hipEvent_t* e) {
     EventPool* p = sc->pool;
     if (p->n <= 0) return LGCN_EINVAL;
-    if (p->next >= p->n) p->next = 0;
+    if (p->next >= p->n) return LGCN_ETOOMANY;
     *e = p->ev[p->next++];
     return 0;
 }
@@ -1073,6 +1130,9 @@ struct Deps {
     hipEvent_t part_wait[2] = {nullptr, nullptr};
     bool defer = false;
     hipEvent_t part_done[2] = {nullptr, nullptr};
+    // lk: the layer kernel (and its chunk combine) runs on this stream, forked from and joined
+    // back into `s` (a normal-priority stream for a high-priority lane's last layer kernel)
+    hipStream_t lk = nullptr;
 };
 
 int wait_late(hipStream_t st, const Deps* dp, bool emu = true) {
@@ -1288,7 +1348,13 @@ int plan_layer(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* r
     // wait measured the same, 12.40 / 12.68 vs 12.38 / 12.64 ms)
     if (parts[0].b1 > parts[0].b0)
         if (int e = link(sc, aux_of(0), s)) return e;
-    if (int e = layer_kernel(s)) return e;
+    if (dp && dp->lk && dp->lk != s) {
+        if (int e = link(sc, s, dp->lk)) return e;
+        if (int e = layer_kernel(dp->lk)) return e;
+        if (int e = link(sc, dp->lk, s)) return e;
+    } else if (int e = layer_kernel(s)) {
+        return e;
+    }
     if (int e = mark(3, s)) return e;
     if (chains) {
         if (int e = chain_rows(aux_of(2))) return e;
@@ -1518,6 +1584,13 @@ int run_sides(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* ro
                 dp.part_wait[1] = ab[k - 1];
             }
             dp.defer = k < K && sched && !cap;
+            // the final mean's side-1 layer kernel (lane 1's last) on lane 0's chain stream at
+            // normal priority: on lane 1's high-priority stream its grid held the dispatcher, and
+            // side 0's mean layer (lane 0, the critical path) started ~1.3 ms after the walk it
+            // waits for; sharing the queues they overlap (round 6: C3 forward -0.25..0.35 ms)
+            if (k == K && mean && sched && sched->lk_normal && two && l1_aux && !cap &&
+                sched->n_aux >= 3)
+                dp.lk = sched->aux[2];
             if (mean && k >= 2) {  // the layer kernel's rows read layer K-1's layer-kernel rows
                 dp.late[0] = rest[k - 1];
                 dp.late_emu[0] = part[k - 1][0];
@@ -1577,6 +1650,7 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
     sc->n_aux = n0;
     sc->chain = 1;
     sc->classes = 1;
+    sc->lk_normal = 1;
     for (int i = 0; i < n0; ++i) sc->aux[i] = reinterpret_cast<hipStream_t>(aux_streams[i]);
     int e = 0;
     for (; pool->n < kPoolEvents && !e; ++pool->n)
@@ -1646,6 +1720,9 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
             return 0;
         case LGCN_SCHED_CLASSES:
             sc->classes = value != 0;
+            return 0;
+        case LGCN_SCHED_LK_NORMAL:
+            sc->lk_normal = value != 0;
             return 0;
         default:
             return LGCN_EINVAL;

@@ -226,8 +226,15 @@ __global__ __launch_bounds__(64) void k_emu_blocks(const lgcn_edge_t* __restrict
             const int col = 8 * i + sub;
             const float4 v = *reinterpret_cast<const float4*>(s_tile + col * TP + 4 * q);
             const int cg = blockIdx.y * 64 + col;
-            if (cg < d)
-                *reinterpret_cast<float4*>(st0 + (int64_t)cg * LGCN_EMU_BLOCK + step0 + 4 * q) = v;
+            // non-temporal: the walk re-reads ~10% of the stage, much later; streaming stores
+            // keep the layer kernels' gathered rows in L2 / MALL (round 6: forward -0.15..0.4 ms,
+            // BPR backward -0.1 ms, A/B on one box)
+            if (cg < d) {
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(
+                    f4v{v.x, v.y, v.z, v.w},
+                    reinterpret_cast<f4v*>(st0 + (int64_t)cg * LGCN_EMU_BLOCK + step0 + 4 * q));
+            }
         }
         wave_sync();
     };

@@ -55,15 +55,66 @@ def shutdown():
 # ----------------------------------------------------------------------------------------------
 # row partition planning (host)
 # ----------------------------------------------------------------------------------------------
-def balanced_row_bounds(deg, world, row_cost=4.0):
-    """Contiguous row blocks with near-equal (nnz + row_cost * rows): P+1 boundaries."""
+# a walked row (above the chain cut: block pass + walk, one wave per column) costs its rank
+# ~20x a bandwidth-bound edge: the C3 2.77M-edge item row's walk takes ~3.0 ms alone while a layer
+# kernel moves ~18 edges/ns
+WALK_FACTOR = 20.0
+
+
+def row_costs(deg, row_cost=4.0, walk_deg=None, walk_factor=WALK_FACTOR):
+    """Per-row cost of a rank's exact-plan layer: nnz + row_cost for the rows the layer kernel
+    and the chain kernel run, walk_factor x nnz for the walked rows (degree > walk_deg)."""
     deg = np.asarray(deg, dtype=np.float64)
-    n = deg.size
-    cum = np.concatenate([[0.0], np.cumsum(deg + row_cost)])
-    targets = cum[-1] * np.arange(world + 1) / world
-    b = np.searchsorted(cum, targets, side="left").astype(np.int64)
-    b[0], b[-1] = 0, n
-    return np.maximum.accumulate(np.minimum(b, n))
+    cost = deg + row_cost
+    if walk_deg is not None:
+        w = deg > walk_deg
+        cost[w] = deg[w] * walk_factor + row_cost
+    return cost
+
+
+def _equal_cost_bounds(cum, lo, hi, k):
+    """k contiguous blocks of rows [lo, hi) with near-equal cost (cum: prefix sums of the costs)."""
+    t = cum[lo] + (cum[hi] - cum[lo]) * np.arange(k + 1) / k
+    b = np.searchsorted(cum, t, side="left").astype(np.int64)
+    b[0], b[-1] = lo, hi
+    return np.maximum.accumulate(np.clip(b, lo, hi))
+
+
+def balanced_row_bounds(deg, world, row_cost=4.0, walk_deg=None, walk_factor=WALK_FACTOR):
+    """Contiguous row blocks of near-equal cost (row_costs: nnz + row_cost per row, walked rows
+    at walk_factor x nnz): P+1 boundaries. A row costing more than a rank's share (a walked hub
+    row) gets a rank of its own when the ranks allow it, and the rows between such rows share the
+    other ranks in proportion to their cost — so the rank that owns the 2.77M-edge row carries no
+    other rows (rowpart balanced by walk cost)."""
+    cost = row_costs(deg, row_cost, walk_deg, walk_factor)
+    n = cost.size
+    if world <= 1 or n == 0:
+        return np.asarray([0] + [n] * world, dtype=np.int64)
+    cum = np.concatenate([[0.0], np.cumsum(cost)])
+    giants = np.flatnonzero(cost > cum[-1] / world)
+    # the non-giant row ranges between the giants
+    edges_ = np.concatenate([[-1], giants, [n]])
+    segs = [(int(a) + 1, int(b)) for a, b in zip(edges_[:-1], edges_[1:]) if b > a + 1]
+    spare = world - giants.size
+    if giants.size == 0 or spare < len(segs):
+        return _equal_cost_bounds(cum, 0, n, world)
+    # ranks per segment: at least 1, the rest by cost (largest remainder), capped by its rows
+    sc = np.asarray([cum[b] - cum[a] for a, b in segs])
+    k = np.ones(len(segs), dtype=np.int64)
+    for _ in range(spare - len(segs)):
+        room = np.asarray([b - a for a, b in segs]) > k
+        if not room.any():
+            break
+        i = int(np.argmax(np.where(room, sc / k, -1.0)))
+        k[i] += 1
+    b = [0]
+    pieces = sorted([(a, b_, int(kk)) for (a, b_), kk in zip(segs, k)] +
+                    [(int(g), int(g) + 1, 1) for g in giants])
+    for a, b_, kk in pieces:
+        b.extend(_equal_cost_bounds(cum, a, b_, kk)[1:].tolist())
+    while len(b) < world + 1:  # fewer rows than ranks somewhere: empty trailing blocks
+        b.append(n)
+    return np.asarray(b, dtype=np.int64)
 
 
 def layout_positions(bounds, n_max, ids):
@@ -85,9 +136,12 @@ def feature_bounds(d, world):
 class RowPartPlan:
     """Rank-local row block of a row-sorted global COO (r, c, v) with n nodes."""
 
-    def __init__(self, r, c, v, n, world, rank, device, row_cost=4.0):
+    def __init__(self, r, c, v, n, world, rank, device, row_cost=4.0, walk_deg="auto"):
         rowptr_g = np.searchsorted(r, np.arange(n + 1)).astype(np.int64)
-        self.bounds = balanced_row_bounds(np.diff(rowptr_g), world, row_cost)
+        if walk_deg == "auto":  # the engine's chain cut for the whole graph: rows above it walk
+            walk_deg = engine.chain_max_degree(len(v)) if torch.device(device).type == "cuda" \
+                else None
+        self.bounds = balanced_row_bounds(np.diff(rowptr_g), world, row_cost, walk_deg)
         self.n, self.world, self.rank, self.device = n, world, rank, device
         self.n_max = int(np.diff(self.bounds).max())
         self.r0, self.r1 = int(self.bounds[rank]), int(self.bounds[rank + 1])

@@ -29,13 +29,14 @@ SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, S
     1, 2, 3, 4, 5, 6
 SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
 SCHED_CLASSES = 16
+SCHED_LK_NORMAL = 17
 SCHED_STATE_LANES, SCHED_STATE_L1_AUX, SCHED_STATE_CAPTURING, SCHED_STATE_CLASSES = 1, 2, 3, 4
 # segments of a sided propagation: the three side-0 classes, then side 1
 N_SEGS = 4
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
 TRACE_PHASES = ("start", "part0_blocks", "part1_blocks", "layer_kernel", "chain_rows",
                 "part0_walk", "part1_walk", "joined")
-ABI_VERSION = 13
+ABI_VERSION = 14
 LGCN_EMU_CANDS, LGCN_EMU_META_BYTES, LGCN_EMU_BLOCK = 16, 16, 256
 
 # Rows up to this degree run as row bundles in the layer kernel (one sequential fmaf chain each,
@@ -101,11 +102,11 @@ def chain_max_degree(nnz, backward=False):
     return int(f(int(nnz)))
 
 
-# Edges per hub chunk: LGCN_HUB_CHUNK, else by graph size (hub_chunk_for). A chunk is one lane
-# group's sequential chain, so it must stay short against the whole layer: on the C2 graph
-# (1.6M nonzeros, 0.07-0.1 ms per layer) 128-edge chunks run the forward 0.318 -> 0.224 ms,
-# on C3 (56M) 256 is best (tools/tune.py).
-DEFAULT_HUB_CHUNK = int(os.environ.get("LGCN_HUB_CHUNK", "0")) or None
+# Edges per hub chunk (chunk mode): DEFAULT_HUB_CHUNK when set (tests, tools/tune.py), else by
+# graph size (hub_chunk_for). A chunk is one lane group's sequential chain, so it must stay short
+# against the whole layer: on the C2 graph (1.6M nonzeros, 0.07-0.1 ms per layer) 128-edge
+# chunks run the forward 0.318 -> 0.224 ms, on C3 (56M) 256 is best (tools/tune.py).
+DEFAULT_HUB_CHUNK = None
 
 
 def hub_chunk_for(nnz):
@@ -113,7 +114,7 @@ def hub_chunk_for(nnz):
         return DEFAULT_HUB_CHUNK
     return 256 if nnz >= 8_000_000 else 128
 # Hub rows with more chunks than this are combined in two levels (plan_hubs); 0 = one level
-DEFAULT_HUB_PRE_GROUP = int(os.environ.get("LGCN_HUB_PRE_GROUP", "256"))
+DEFAULT_HUB_PRE_GROUP = 256
 
 
 class RowsT(ctypes.Structure):
@@ -162,6 +163,8 @@ ABI = [
     ("lgcn_error_string", ctypes.c_char_p, [ctypes.c_int]),
     ("lgcn_tune", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("lgcn_device_info", ctypes.c_int, [ctypes.c_int, _P, _P]),
+    ("lgcn_stream_create_dedicated", ctypes.c_int, [_P]),
+    ("lgcn_stream_destroy", ctypes.c_int, [_P]),
     ("lgcn_coo_inspect", ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
     ("lgcn_coo_to_csr", ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P]),
     ("lgcn_coo_sort_perm", ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P,
@@ -248,13 +251,6 @@ def load_library(path=None):
             fn.argtypes = args
         if lib.lgcn_abi_version() != ABI_VERSION:
             raise LgcnError("liblgcn_engine.so ABI version mismatch")
-        # LGCN_MEAN_PREFETCH=off: A/B switch of the MEAN layer's bundle prefetch (same bits)
-        if os.environ.get("LGCN_MEAN_PREFETCH", "").lower() in ("0", "off"):
-            lib.lgcn_tune(TUNE_MEAN_PREFETCH, 2)
-        # LGCN_EMU_MARGIN=shift:base: A/B of the walk's prediction margin (same bits)
-        if os.environ.get("LGCN_EMU_MARGIN", ""):
-            sh, base = (int(t) for t in os.environ["LGCN_EMU_MARGIN"].split(":"))
-            lib.lgcn_tune(TUNE_EMU_MARGIN, (base << 4) | sh)
         _lib = lib
         return lib
 
@@ -787,11 +783,9 @@ def side_classes(lib, g, stream):
 
 def sides_min_nnz():
     """Graphs from this many nonzeros run the bipartite schedule when the caller names the sides
-    (LGCN_SIDES_MIN_NNZ, default 2^23; LGCN_SIDES=0 turns it off): below it a layer is a few
-    short launches and splitting them into half-layers on 8 streams only adds latency (C2,
-    1.6M nonzeros: forward 1.54 ms with the two lanes, 1.10 ms without)."""
-    if os.environ.get("LGCN_SIDES", "1") == "0":
-        return None
+    (LGCN_SIDES_MIN_NNZ, default 2^23): below it a layer is a few short launches and splitting
+    them into half-layers on 8 streams only adds latency (C2, 1.6M nonzeros: forward 1.54 ms
+    with the two lanes, 1.10 ms without)."""
     return int(os.environ.get("LGCN_SIDES_MIN_NNZ", str(1 << 23)))
 
 
@@ -986,15 +980,24 @@ def _check_emb(segments, d, device):
 _scheds = {}
 
 
-def _side_stream(device, i=0, high=False):
+def _side_stream(device, i=0, high=False, dedicated=False):
     """Per-device side streams the emulated and chain rows run on beside the layer kernel
     (lgcn_sched), one per (index, priority); high = created at high priority, so their waves are
-    dispatched first (LGCN_EMU_PRIORITY=0: every stream normal)."""
+    dispatched first; dedicated = normal priority on a hardware queue of its own
+    (lgcn_stream_create_dedicated, wrapped as a torch.cuda.ExternalStream)."""
     sc = _scheds.setdefault(("streams", str(device)), {})
-    high = high and os.environ.get("LGCN_EMU_PRIORITY", "1") != "0"
-    if (i, high) not in sc:
-        sc[(i, high)] = torch.cuda.Stream(device, priority=-1 if high else 0)
-    return sc[(i, high)]
+    key = (i, high, dedicated)
+    if key not in sc:
+        if dedicated:
+            lib = load_library()
+            h = ctypes.c_void_p()
+            with torch.cuda.device(device):
+                _check(lib.lgcn_stream_create_dedicated(ctypes.byref(h)),
+                       "lgcn_stream_create_dedicated")
+            sc[key] = torch.cuda.ExternalStream(h.value, device=device)
+        else:
+            sc[key] = torch.cuda.Stream(device, priority=-1 if high else 0)
+    return sc[key]
 
 
 def _stream_priorities(n_aux, role="forward"):
@@ -1039,7 +1042,11 @@ class Sched:
     def __init__(self, device, n_aux, role="forward"):
         lib = load_library()
         self.lib, self.device, self.n_aux = lib, device, n_aux
-        self.streams = [_side_stream(device, i, hi)
+        # the backward's lane 1 at normal priority: streams with queues of their own, so the
+        # two lanes' 8 normal-priority streams do not take turns on HIP's 4 shared queues
+        ded = role == "backward" and n_aux >= 4 and \
+            os.environ.get("LGCN_DEDICATED_Q", "0") == "1"
+        self.streams = [_side_stream(device, i, hi, ded and i >= 3)
                         for i, hi in enumerate(_stream_priorities(n_aux, role))]
         arr = (ctypes.c_void_p * n_aux)(*[st.cuda_stream for st in self.streams])
         h = ctypes.c_void_p()
@@ -1076,8 +1083,9 @@ def sched_for(device, n_aux=None, role="forward"):
     if not emu_overlap_enabled():
         return None
     # role "backward": lane 1 at normal priority on four streams of its own (_backward_role)
-    key = (str(device), n_aux or n_aux_streams(), emu_slots_key(), chain_enabled(),
-           os.environ.get("LGCN_SCHED_CLASSES", ""), role)
+    key = (str(device), n_aux or n_aux_streams(), chain_enabled(),
+           os.environ.get("LGCN_SCHED_CLASSES", ""), os.environ.get("LGCN_DEDICATED_Q", ""),
+           role)
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1], role)
     return _scheds[key]
@@ -1095,15 +1103,10 @@ def _aligned16(segments):
 
 
 def emu_slots():
-    """LDS slots of the walk (part 0, part 1): env LGCN_EMU_SLOTS="a,b" (default 20,8 — the
-    longest rows run few waves and take many slots; part 1's rows are more waves, and fewer
-    slots fit more of them per CU; C3 forward 20.0 ms at 28,12 -> 19.2 ms at 20,8)."""
-    v = [int(t) for t in os.environ.get("LGCN_EMU_SLOTS", "20,8").split(",") if t.strip()]
-    return v or [0]
-
-
-def emu_slots_key():
-    return os.environ.get("LGCN_EMU_SLOTS", "")
+    """LDS slots of the walk (part 0, part 1): 20, 8 — the longest rows run few waves and take
+    many slots; part 1's rows are more waves, and fewer slots fit more of them per CU (C3
+    forward 20.0 ms at 28,12 -> 19.2 ms at 20,8; 20,4 / 16,6 the same or worse, round 4)."""
+    return [20, 8]
 
 
 def emu_overlap_enabled():
@@ -1353,11 +1356,74 @@ def _sparse_grad_mode():
     return m
 
 
-_live_hint = {}  # device -> [slots, events, next slot, last role]: recent live-row counts
+_live_hint = {}  # device -> [slots, events, scales, next slot, last role]: recent live-row counts
 _HINT_SLOTS = 8
+_HINT_SAMPLE = 64  # a dense-path call counts the live rows of every 64th row of G (an estimate)
 
 
-def _backward_role(dev, n, cnt):
+def _hint_entry(dev):
+    key = str(dev)
+    h = _live_hint.get(key)
+    if h is None:
+        h = [torch.empty(_HINT_SLOTS, dtype=torch.int32, pin_memory=True),
+             [None] * _HINT_SLOTS, [1] * _HINT_SLOTS, 0, "forward"]
+        _live_hint[key] = h
+    return h
+
+
+def _hint_latest(dev):
+    """The newest landed live-row count of G (scaled up when sampled), or None."""
+    slots, evs, scales, nxt, _ = _hint_entry(dev)
+    for k in range(1, _HINT_SLOTS + 1):   # newest first
+        i = (nxt - k) % _HINT_SLOTS
+        if evs[i] is not None and evs[i].query():
+            return int(slots[i]) * scales[i]
+    return None
+
+
+def _hint_push(dev, cnt, scale=1):
+    """Copy the device count `cnt` into the next pinned slot, asynchronously."""
+    h = _hint_entry(dev)
+    slots, evs, scales, nxt, _ = h
+    slot = nxt % _HINT_SLOTS
+    slots[slot:slot + 1].copy_(cnt.view(-1)[:1], non_blocking=True)
+    if evs[slot] is None:
+        evs[slot] = torch.cuda.Event()
+    evs[slot].record()
+    scales[slot] = scale
+    h[3] = nxt + 1
+
+
+def _hint_dense(dev, n):
+    """True when the newest landed count says G was dense (>= n/8 live rows) — the mask would
+    mark every row, so the backward skips it and runs the dense kernels (round 6: dense backward
+    16.4 -> see DESIGN §4e). False before any count has landed and under a capture."""
+    if os.environ.get("LGCN_DENSE_SKIP_MASK", "1") == "0":
+        return False
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    c = _hint_latest(dev)
+    return c is not None and c * 8 >= n
+
+
+def _sampled_live_count(segs, d, dev):
+    """Device count of the live rows among every _HINT_SAMPLE-th row of G (lgcn_rows_nonzero over
+    strided views of the blocks: ~1/64 of G's bytes), for the next call's choice."""
+    S = _HINT_SAMPLE
+    views = [t[::S] for t in segs if t.shape[0] > 0]
+    if not views:
+        return None
+    lib = load_library()
+    n = sum(int(v.shape[0]) for v in views)
+    mask = torch.empty(max((n + 31) // 32, 1), dtype=torch.int32, device=dev)
+    count = torch.empty(1, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib.lgcn_rows_nonzero(rows_desc(views, S * d), n, d, _ptr(mask), _ptr(count),
+                                     _stream(dev)), "lgcn_rows_nonzero")
+    return count
+
+
+def _backward_role(dev, n, cnt, scale=1):
     """Which schedule a sided backward runs on. A row-sparse G (a BPR batch: live-edge chains
     instead of walks) runs fastest with both lanes at normal priority, a dense G (walks of the
     hub rows) with lane 1 high as the forward (round 5: BPR-batch backward 9.7 -> 9.0 ms, dense
@@ -1366,28 +1432,15 @@ def _backward_role(dev, n, cnt):
     has landed (a training loop's gradients keep their sparsity from step to step); with none
     landed the previous choice stays (the forward's schedule at first and under a HIP-graph
     capture). Same bits either way."""
-    if os.environ.get("LGCN_BWD_NORMAL", "auto") == "0" or cnt is None:
+    if cnt is None:
         return "forward"
     if torch.cuda.is_current_stream_capturing():
         return "forward"
-    key = str(dev)
-    h = _live_hint.get(key)
-    if h is None:
-        h = [torch.empty(_HINT_SLOTS, dtype=torch.int32, pin_memory=True),
-             [None] * _HINT_SLOTS, 0, "forward"]
-        _live_hint[key] = h
-    slots, evs, nxt, role = h
-    for k in range(1, _HINT_SLOTS + 1):   # newest first
-        i = (nxt - k) % _HINT_SLOTS
-        if evs[i] is not None and evs[i].query():
-            role = "backward" if int(slots[i]) * 8 < n else "forward"
-            break
-    slot = nxt % _HINT_SLOTS
-    slots[slot:slot + 1].copy_(cnt.view(-1)[:1], non_blocking=True)
-    if evs[slot] is None:
-        evs[slot] = torch.cuda.Event()
-    evs[slot].record()
-    h[2], h[3] = nxt + 1, role
+    h = _hint_entry(dev)
+    latest = _hint_latest(dev)
+    role = h[4] if latest is None else ("backward" if latest * 8 < n else "forward")
+    _hint_push(dev, cnt, scale)
+    h[4] = role
     return role
 
 
@@ -1420,15 +1473,21 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
             return out
         mode = sparse or _sparse_grad_mode()
         nz = cnt = None
+        scale = 1
         if mode in ("auto", "on") and n > 0:
-            # no host decision (a read-back would sync every step): the mask costs one pass over
-            # G (0.7 ms at C3) and a dense G runs the masked kernels at the dense rate
-            nz, cnt = rows_nonzero(segs, d, dev)
+            # no host read-back (it would sync every step): the mask costs one pass over G (0.7 ms
+            # at C3). When the previous calls' counts say G is dense, the mask would mark every
+            # row: skip it (and the live-edge path it gates) and only sample G's rows for the
+            # next call's choice
+            if mode == "auto" and _hint_dense(dev, n):
+                cnt, scale = _sampled_live_count(segs, d, dev), _HINT_SAMPLE
+            else:
+                nz, cnt = rows_nonzero(segs, d, dev)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
         if use_sides(gt):
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
                                    live=nz is not None, backward=True)
-            sc = sched_for(dev, role=_backward_role(dev, n, cnt))
+            sc = sched_for(dev, role=_backward_role(dev, n, cnt, scale))
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             sides = gt.sides_struct()
             try:
@@ -1442,6 +1501,8 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
             _note_schedule(sc, gt)
             _collect_sides(ev, K, gt)
             return out
+        if cnt is not None and not torch.cuda.is_current_stream_capturing():
+            _hint_push(dev, cnt, scale)
         hp = gt.hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
         ep = _epilogue(LGCN_EPI_ADD, addend=g, div=float(K + 1))
         ep.addend_nz = None if nz is None else nz.data_ptr()
@@ -1525,6 +1586,11 @@ class PropagateFunction(torch.autograd.Function):
             if g.dtype != torch.float32 or g.shape != blk.shape or g.device != blk.device:
                 raise LgcnError(f"ego gradient {tuple(g.shape)} {g.dtype} does not match its "
                                 f"block {tuple(blk.shape)}")
+            if ctx.K == 0:
+                # dE0 is G itself here and may hold -0, where autograd's dense sum with the
+                # alias gradient's +0 gives +0: the plain add
+                blk.add_(g)
+                continue
             with torch.cuda.device(dev):
                 _check(lib.lgcn_add_nonzero(_ptr(g), _ptr(blk), g.numel(), _stream(dev)),
                        "lgcn_add_nonzero")

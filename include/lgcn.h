@@ -43,12 +43,13 @@
 extern "C" {
 #endif
 
-#define LGCN_ABI_VERSION 13
+#define LGCN_ABI_VERSION 14
 
 /* engine error codes (negative; positive values are hipError_t) */
 #define LGCN_EINVAL      (-1)   /* bad size / null pointer / unsupported dimension */
 #define LGCN_EALIGN      (-2)   /* a vectorised path needs 16-B aligned rows; see engine.py */
-#define LGCN_ETOOMANY    (-3)   /* more than LGCN_MAX_LAYERS previous layers in a mean epilogue */
+#define LGCN_ETOOMANY    (-3)   /* more than LGCN_MAX_LAYERS previous layers in a mean epilogue,
+                                   or a schedule's event pool exhausted by one call */
 
 #define LGCN_MAX_LAYERS 16      /* torch.mean over <= 17 stacked layers sums them sequentially */
 
@@ -256,6 +257,14 @@ int lgcn_tune(int knob, int value);
 /* device properties the host side needs (CU count); returns 0/hipError */
 int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host);
 
+/* A normal-priority stream with a hardware queue of its own on the current device: HIP serves
+ * streams from a pool of GPU_MAX_HW_QUEUES queues per priority (default 4), and two streams on
+ * one queue run in order — a schedule with more than four normal-priority streams (the
+ * backward's two lanes at normal priority: 8) serialises on the shared queues. A stream created
+ * with a CU mask always gets a new queue; every CU is enabled (no placement restriction). */
+int lgcn_stream_create_dedicated(void** stream);
+int lgcn_stream_destroy(void* stream);
+
 /* ---- graph preparation (replaces the per-call COO handling inside torch.sparse.mm) ---------- */
 
 /* Inspect a COO (rows/cols int64, as torch.sparse_coo_tensor._indices()) and OR LGCN_COO_*
@@ -326,7 +335,9 @@ int lgcn_csr_relabel_cols(const lgcn_edge_t* edges, int64_t nnz, const int32_t* 
  * part_rows0) are the rows of the side-1 plans' walked part 0 (the longest item rows), [split +
  * part_rows0, split + part_rows1) part 1 — a degree-ordered plan lists its emulated rows in slot
  * order, so these are the first slots of side 1. A side-0 row is class 0 if it is linked to a
- * part-0 row, class 1 if linked to a part-1 row only, class 2 otherwise. Writes the same operator
+ * part-0 row, class 1 if linked to a part-1 row only, class 2 otherwise — linked in either
+ * direction (the part row reads it, or it reads the part row), so the classes also hold for an
+ * operator that is not structurally symmetric. Writes the same operator
  * with side 0's slots stably re-sorted by class (each class keeps its degree order; side 1 is
  * unchanged): row_ids_out / rowptr_out / edges_out as lgcn_csr_order_by_degree's, and
  * class_end[0..1] (device int32[2]) = the first slot of class 1 and of class 2. Bitwise-neutral
@@ -503,6 +514,10 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        and lets side 1's walked parts wait only for the classes
                                        they read (lgcn_sides_t); 0: every part waits for the
                                        whole side-0 half-layer before it (same bits) */
+#define LGCN_SCHED_LK_NORMAL    17  /* 1 (default): the final mean's side-1 layer kernel (lane
+                                       1's last) runs on aux_streams[2] at normal priority, so the
+                                       side-0 mean overlaps it instead of waiting for its grid;
+                                       0: on lane 1's main stream (same bits) */
 /* (under a HIP-graph capture lane 1 runs its half-layers on its main stream alone: DESIGN §4d) */
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 /* What the latest lgcn_propagate_*_sides call on this schedule ran (diagnostics, tests). */

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_version_and_errors(lib):
-    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 13
+    assert lib.lgcn_abi_version() == engine.ABI_VERSION == 14
     assert b"invalid" in lib.lgcn_error_string(-1)
     assert lib.lgcn_error_string(0) == b"success"
 

@@ -127,6 +127,21 @@ def test_balanced_bounds_and_layout():
         assert len(np.unique(pos)) == len(deg)
         owner = pos // n_max
         assert np.all(np.diff(owner) >= 0)
+    # walk cost: the rank holding a walked hub row gets few other rows, every rank some
+    rng = np.random.default_rng(0)
+    deg = rng.integers(1, 40, 10_000)
+    deg[3_000] = 30_000   # below a rank's share by nnz, far above it as a walk
+    for world in (4, 8):
+        b0 = D.balanced_row_bounds(deg, world)
+        b1 = D.balanced_row_bounds(deg, world, walk_deg=20_000)
+        assert len(b1) == world + 1 and b1[0] == 0 and b1[-1] == deg.size
+        assert np.all(np.diff(b1) >= 1)
+        own0 = np.searchsorted(b0, 3_000, side="right") - 1
+        own1 = np.searchsorted(b1, 3_000, side="right") - 1
+        assert np.diff(b1)[own1] == 1 < np.diff(b0)[own0]   # the walked row alone
+        cost = D.row_costs(deg, walk_deg=20_000)
+        blk = [cost[b1[i]:b1[i + 1]].sum() for i in range(world) if i != own1]
+        assert max(blk) <= 1.15 * (cost.sum() - cost[3_000]) / (world - 1)
     cb = D.feature_bounds(64, 8)
     assert list(np.diff(cb)) == [8] * 8
     cb = D.feature_bounds(12, 8)

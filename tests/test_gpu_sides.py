@@ -62,9 +62,10 @@ def _classes_env(monkeypatch, classes):
         monkeypatch.setenv("LGCN_SCHED_CLASSES", "0")
 
 
-def _check_classes(g, r, c, n):
+def _check_classes(g, r, c, n, both=False):
     """The class-major slot order: side 0 = users + brands in classes 0 / 1 / 2 by the walked
-    item rows they link to, each class degree-descending; side 1 untouched."""
+    item rows they link to, each class degree-descending; side 1 untouched. both: linked in
+    either direction (an operator that is not structurally symmetric)."""
     ids = g.row_ids.cpu().numpy()
     rp = g.rowptr_host().astype(np.int64)
     deg = np.diff(rp)
@@ -77,6 +78,8 @@ def _check_classes(g, r, c, n):
         for s_ in range(a, b, max(1, (b - a) // 200)):   # a sample of each class
             row = ids[s_]
             nb = c[np.searchsorted(r, row):np.searchsorted(r, row + 1)]
+            if both:
+                nb = np.concatenate([nb, r[c == row]])
             got = min([part[int(x)] for x in nb if int(x) in part], default=2)
             assert got == cls, (s_, row, got, cls)
 
@@ -122,6 +125,61 @@ def test_sides_bitwise(gpu_device, monkeypatch, brand_graph, n_aux, kind, classe
             got_b = engine.propagate_backward(g, _segs(G, gpu_device), K, sparse=sparse,
                                               **KW).cpu().numpy()
             assert np.array_equal(got_b.view(np.uint32), want_b.view(np.uint32)), (K, sparse)
+
+
+def test_classes_directed_operator(gpu_device, monkeypatch, brand_graph):
+    """the side-0 classes of an operator that is bipartite but not structurally
+    symmetric. Half of the item -> user edges are dropped, so many users read a walked item row
+    that does not read them; lgcn_csr_side_classes marks classes from both directions, and the
+    class schedule (classes on, two lanes with their aux streams) stays bitwise."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
+    _classes_env(monkeypatch, "on")
+    r, c, v, n = brand_graph
+    rng = np.random.default_rng(3)
+    drop = (r >= U) & (r < U + I) & (c < U) & (rng.random(r.size) < 0.5)
+    r, c, v = r[~drop], c[~drop], v[~drop]
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    assert g.split == n - I
+    _check_classes(g, r, c, n, both=True)
+    e0 = _e0(rng, "xavier", n, 64)
+    for K in (2, 3):
+        got = engine.propagate_forward(g, _segs(e0, gpu_device), K, **KW).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), oracle.forward(r, c, v, e0, K).view(np.uint32))
+        assert engine.last_schedule["classes"]
+    G = _e0(rng, "xavier", n, 64)
+    got_b = engine.propagate_backward(g, _segs(G, gpu_device), 3, sparse="off", **KW)
+    assert np.array_equal(got_b.cpu().numpy().view(np.uint32),
+                          oracle.backward(r, c, v, G, 3).view(np.uint32))
+
+
+def test_dedicated_queue_streams_bitwise(gpu_device, monkeypatch, brand_graph):
+    """lgcn_stream_create_dedicated: the backward's lane 1 on normal-priority streams with queues
+    of their own (LGCN_DEDICATED_Q=1) — a working stream (torch work on it completes) and the
+    same bits as the oracle."""
+    from gcn_recommendation_amd import engine as E
+    lib = E.load_library()
+    h = __import__("ctypes").c_void_p()
+    with torch.cuda.device(gpu_device):
+        assert lib.lgcn_stream_create_dedicated(__import__("ctypes").byref(h)) == 0
+    st = torch.cuda.ExternalStream(h.value, device=gpu_device)
+    with torch.cuda.stream(st):
+        x = torch.arange(1 << 20, device=gpu_device, dtype=torch.float32).sum()
+    st.synchronize()
+    assert float(x) == float((1 << 20) * ((1 << 20) - 1) // 2)
+    assert lib.lgcn_stream_destroy(h) == 0
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
+    monkeypatch.setenv("LGCN_DEDICATED_Q", "1")
+    r, c, v, n = brand_graph
+    g = E.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    rng = np.random.default_rng(9)
+    G = _e0(rng, "xavier", n, 64)
+    G[rng.random(n) > 0.02] = 0.0
+    want = oracle.backward(r, c, v, G, 3)
+    for _ in range(3):   # the row-sparse schedule (role "backward") once the hint has landed
+        got = E.propagate_backward(g, _segs(G, gpu_device), 3, **KW).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
 def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):

@@ -80,6 +80,35 @@ def test_ego_alias_gradients_bitwise(gpu_device, dense):
         assert torch.equal(x.view(torch.int32), y.view(torch.int32))
 
 
+def test_ego_alias_k0_negative_zero(gpu_device):
+    """n_layers = 0: dE0 is G itself and may hold -0; where the ego alias's gradient
+    is +0, autograd's sum gives +0 — the aliases' backward must too."""
+    from gcn_recommendation_amd import engine
+    z = load_case("c1_brand")
+    U, I, B, d, _ = case_dims(z)
+    adj = graph.build_norm_adj(z["train_user"], z["train_item"], U, I, B, z["ib_item"],
+                               z["ib_brand"], bool(z["use_brand"]), device=gpu_device)
+    g = torch.Generator().manual_seed(4)
+    G = [torch.randn(n, d, generator=g) for n in (U, I, B)]
+    E = [torch.randn(n, d, generator=g) for n in (U, I)]
+    for t in G:
+        t[torch.rand(t.shape, generator=g) < 0.3] = -0.0
+    for t in E:
+        t[torch.rand(t.shape, generator=g) < 0.5] = 0.0
+    G = [t.to(gpu_device) for t in G]
+    E = [t.to(gpu_device) for t in E]
+    res = []
+    for e0_outputs in (2, 0):
+        torch.manual_seed(7)
+        w = [torch.randn(n, d, device=gpu_device).requires_grad_() for n in (U, I, B)]
+        out = engine.propagate_blocks(adj, w, 0, e0_outputs=e0_outputs)
+        ego = list(out[3:]) if e0_outputs else [w[0], w[1]]
+        torch.autograd.backward(list(out[:3]) + ego, G + E)
+        res.append([t.grad.clone() for t in w])
+    for x, y in zip(*res):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
 def test_add_nonzero_matches_dense_add(gpu_device):
     """lgcn_add_nonzero == dst + src bitwise for dst != -0 (zeros of both signs, NaN, inf, odd
     lengths and a misaligned start take the scalar path)."""

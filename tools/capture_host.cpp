@@ -1,0 +1,244 @@
+// C host (no torch, no Python in the process) capturing the library's own sided forward into a
+// HIP graph: the discriminating run for the capture crash of DESIGN §4d.
+// The graph (a bipartite user-item operator with walked item rows), the plans (the C planner:
+// lgcn_plan_exact / lgcn_plan_scratch_bytes per segment) and the 7-stream
+// schedule are built as a C host builds them; then
+//   1. one eager lgcn_propagate_forward_sides (and _backward_sides) -> reference outputs;
+//   2. the same calls between hipStreamBeginCapture / hipStreamEndCapture on the caller's
+//      stream, hipGraphInstantiate, two hipGraphLaunch-es over NaN-filled outputs;
+//   3. the replays compared bitwise with the eager outputs; lgcn_sched_state reports how many
+//      aux streams lane 1 ran on under the capture (3 with the LGCN_CAPTURE_AUX_EXP library).
+// A SIGSEGV prints the native backtrace (execinfo) before the process dies.
+//   hipcc --offload-arch=gfx950 -O2 -I include tools/capture_host.cpp \
+//     -L <dir> -l<lgcn_engine | lgcn_capaux> -Wl,-rpath,<dir> -o tools/capture_host
+#include <execinfo.h>
+#include <hip/hip_runtime.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <random>
+#include <vector>
+
+#include "lgcn.h"
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+#define CL(x)                                                                                  \
+    do {                                                                                       \
+        int r_ = (x);                                                                          \
+        if (r_ != 0) {                                                                         \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, lgcn_error_string(r_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+static void on_segv(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    fprintf(stderr, "signal %d, native backtrace:\n", sig);
+    backtrace_symbols_fd(fr, n, 2);
+    _exit(128 + sig);
+}
+
+template <class T>
+static T* dev_copy(const std::vector<T>& h) {
+    T* p = nullptr;
+    CK(hipMalloc(&p, std::max<size_t>(h.size(), 1) * sizeof(T)));
+    if (!h.empty()) CK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return p;
+}
+
+static void* dev_alloc(size_t bytes) {
+    void* p = nullptr;
+    CK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+    return p;
+}
+
+int main(int argc, char** argv) {
+    signal(SIGSEGV, on_segv);
+    signal(SIGABRT, on_segv);
+    const int U = 60000, I = 4000, d = 64, K = argc > 1 ? atoi(argv[1]) : 3;
+    const int64_t n_inter = 300000;
+    const int n = U + I;
+    // -- the graph: Zipf item popularity, symmetric normalised adjacency (main.py:282-336 shape)
+    std::mt19937_64 rng(5);
+    std::vector<double> cdf(I);
+    double acc = 0;
+    for (int i = 0; i < I; ++i) cdf[i] = (acc += 1.0 / std::pow(i + 1.0, 1.1));
+    std::vector<std::pair<int, int>> ui;
+    for (int64_t t = 0; t < n_inter; ++t) {
+        const double x = std::uniform_real_distribution<double>(0, acc)(rng);
+        const int it = (int)(std::lower_bound(cdf.begin(), cdf.end(), x) - cdf.begin());
+        ui.emplace_back((int)(rng() % U), it);
+    }
+    std::sort(ui.begin(), ui.end());
+    ui.erase(std::unique(ui.begin(), ui.end()), ui.end());
+    std::vector<std::vector<int>> adj(n);
+    for (auto& e : ui) {
+        adj[e.first].push_back(U + e.second);
+        adj[U + e.second].push_back(e.first);
+    }
+    for (auto& a : adj) std::sort(a.begin(), a.end());
+    // -- slot order: side 0 (users) then side 1 (items), each degree-descending, stable
+    std::vector<int32_t> row_ids(n);
+    std::iota(row_ids.begin(), row_ids.end(), 0);
+    auto by_deg = [&](int32_t a, int32_t b) { return adj[a].size() > adj[b].size(); };
+    std::stable_sort(row_ids.begin(), row_ids.begin() + U, by_deg);
+    std::stable_sort(row_ids.begin() + U, row_ids.end(), by_deg);
+    const int split = U;
+    std::vector<int32_t> rowptr(n + 1, 0);
+    std::vector<lgcn_edge_t> edges;
+    for (int s = 0; s < n; ++s) {
+        const int r = row_ids[s];
+        for (int c : adj[r]) {
+            const float v = 1.0f / std::sqrt((float)adj[r].size() * (float)adj[c].size());
+            uint32_t vb;
+            memcpy(&vb, &v, 4);
+            edges.push_back((lgcn_edge_t)(((uint64_t)vb << 32) | (uint32_t)c));
+        }
+        rowptr[s + 1] = (int32_t)edges.size();
+    }
+    const int64_t nnz = (int64_t)edges.size();
+    // -- plans: 4 segments (side-0 classes 0..2: one class here; side 1), two scratch sets each
+    lgcn_sides_t sides;
+    sides.n = n;
+    sides.split = split;
+    sides.class_end[0] = sides.class_end[1] = split;
+    sides.part_rows[0] = sides.part_rows[1] = 0;
+    const int seg_lo[4] = {0, split, split, split}, seg_hi[4] = {split, split, split, n};
+    const int32_t chain_max = 2048, part0_blocks = 40;   // walked item rows of both parts
+    lgcn_hub_plan_t plans[8];
+    memset(plans, 0, sizeof(plans));
+    for (int g = 0; g < 4; ++g) {
+        const int lo = seg_lo[g], nr = seg_hi[g] - seg_lo[g];
+        lgcn_hub_plan_t base;
+        memset(&base, 0, sizeof(base));
+        base.threshold = 128;
+        std::vector<lgcn_emu_row_t> er;
+        std::vector<lgcn_emu_block_t> eb;
+        if (nr > 0) {
+            CL(lgcn_plan_exact(rowptr.data() + lo, row_ids.data() + lo, nr, 128, chain_max,
+                               part0_blocks, nullptr, nullptr, &base));
+            er.resize(base.n_emu_rows);
+            eb.resize(base.n_emu_blocks);
+            CL(lgcn_plan_exact(rowptr.data() + lo, row_ids.data() + lo, nr, 128, chain_max,
+                               part0_blocks, er.data(), eb.data(), &base));
+        }
+        printf("segment %d: %d rows, %d emulated rows (parts %d / %d), %d blocks\n", g, nr,
+               base.n_emu_rows, base.emu_part_rows[0], base.emu_part_rows[1], base.n_emu_blocks);
+        size_t sz[3] = {0, 0, 0};
+        CL(lgcn_plan_scratch_bytes(&base, d, 0, sz));
+        lgcn_emu_row_t* d_er = er.empty() ? nullptr : dev_copy(er);
+        lgcn_emu_block_t* d_eb = eb.empty() ? nullptr : dev_copy(eb);
+        for (int j = 0; j < 2; ++j) {
+            lgcn_hub_plan_t p = base;
+            p.emu_rows = d_er;
+            p.emu_blocks = d_eb;
+            if (sz[0]) {
+                p.emu_rel = (float*)dev_alloc(sz[0]);
+                p.emu_meta = dev_alloc(sz[1]);
+                p.emu_stage = (float*)dev_alloc(sz[2]);
+            }
+            if (base.n_emu_rows) p.emu_out = (float*)dev_alloc((size_t)base.n_emu_rows * d * 4);
+            plans[2 * g + j] = p;
+        }
+    }
+    // -- device operator, E0 and the outputs
+    int32_t* d_rowptr = dev_copy(rowptr);
+    lgcn_edge_t* d_edges = dev_copy(edges);
+    int32_t* d_ids = dev_copy(row_ids);
+    std::vector<float> e0((size_t)n * d);
+    std::normal_distribution<float> nd(0.f, 0.1f);
+    for (auto& x : e0) x = nd(rng);
+    float* d_e0 = dev_copy(e0);
+    lgcn_rows_t emb = {d_e0, d_e0 + (size_t)U * d, d_e0 + (size_t)U * d, U, n, d};
+    std::vector<float*> layers(std::max(K - 1, 1));
+    for (auto& l : layers) l = (float*)dev_alloc((size_t)n * d * 4);
+    float* d_out = (float*)dev_alloc((size_t)n * d * 4);
+    float* d_gout = (float*)dev_alloc((size_t)n * d * 4);
+    float* d_work = (float*)dev_alloc((size_t)n * d * 4);
+    // -- streams as engine.py creates them: caller + [0..2] normal, lane 1 [3..6] high priority
+    int lo_p = 0, hi_p = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo_p, &hi_p));
+    hipStream_t s, aux[7];
+    CK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, lo_p));
+    for (int i = 0; i < 7; ++i)
+        CK(hipStreamCreateWithPriority(&aux[i], hipStreamNonBlocking, i >= 3 ? hi_p : lo_p));
+    lgcn_sched_t* sc = nullptr;
+    CL(lgcn_sched_create((void* const*)aux, 7, &sc));
+    CL(lgcn_sched_set(sc, LGCN_SCHED_SLOTS0, 20));
+    CL(lgcn_sched_set(sc, LGCN_SCHED_SLOTS1, 8));
+    const lgcn_rows_t gout = {d_out, d_out, d_out, n, n, d};
+    auto forward = [&]() {
+        CL(lgcn_propagate_forward_sides(d_rowptr, d_edges, d_ids, &sides, plans, emb, d, K,
+                                        layers.data(), d_out, sc, s));
+    };
+    auto backward = [&]() {  // Âᵀ = Â (symmetric), G = the forward's output
+        CL(lgcn_propagate_backward_sides(d_rowptr, d_edges, d_ids, &sides, plans, gout, nullptr,
+                                         d, K, d_work, d_gout, sc, s));
+    };
+    // 1. eager reference
+    forward();
+    backward();
+    CK(hipStreamSynchronize(s));
+    std::vector<float> want((size_t)n * d), want_b((size_t)n * d), got((size_t)n * d);
+    CK(hipMemcpy(want.data(), d_out, want.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(want_b.data(), d_gout, want_b.size() * 4, hipMemcpyDeviceToHost));
+    printf("eager: lanes %lld, lane-1 aux streams %lld\n",
+           (long long)lgcn_sched_state(sc, LGCN_SCHED_STATE_LANES),
+           (long long)lgcn_sched_state(sc, LGCN_SCHED_STATE_L1_AUX));
+    fflush(stdout);
+    // 2. capture: forward then backward (the backward reads the forward's output)
+    const char* what = argc > 2 ? argv[2] : "both";
+    hipGraph_t graph;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    if (strcmp(what, "backward") != 0) forward();
+    const long long l1_fwd = (long long)lgcn_sched_state(sc, LGCN_SCHED_STATE_L1_AUX);
+    if (strcmp(what, "forward") != 0) backward();
+    printf("captured (%s): lane-1 aux streams under the capture %lld; ending the capture\n", what,
+           l1_fwd);
+    fflush(stdout);
+    CK(hipStreamEndCapture(s, &graph));
+    size_t n_nodes = 0;
+    CK(hipGraphGetNodes(graph, nullptr, &n_nodes));
+    printf("capture ended: %zu graph nodes\n", n_nodes);
+    fflush(stdout);
+    hipGraphExec_t exec;
+    CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    printf("instantiated\n");
+    fflush(stdout);
+    // 3. replays over NaN-filled outputs, compared bitwise
+    int bad = 0;
+    for (int rep = 0; rep < 2; ++rep) {
+        if (strcmp(what, "backward") != 0) CK(hipMemsetAsync(d_out, 0xff, (size_t)n * d * 4, s));
+        CK(hipMemsetAsync(d_gout, 0xff, (size_t)n * d * 4, s));
+        CK(hipGraphLaunch(exec, s));
+        CK(hipStreamSynchronize(s));
+        if (strcmp(what, "backward") != 0) {
+            CK(hipMemcpy(got.data(), d_out, got.size() * 4, hipMemcpyDeviceToHost));
+            bad += memcmp(got.data(), want.data(), got.size() * 4) != 0;
+        }
+        if (strcmp(what, "forward") != 0) {
+            CK(hipMemcpy(got.data(), d_gout, got.size() * 4, hipMemcpyDeviceToHost));
+            bad += memcmp(got.data(), want_b.data(), got.size() * 4) != 0;
+        }
+    }
+    printf("%s: replays %s (nnz %lld, K %d)\n", what, bad ? "DIFFER" : "bitwise equal to eager",
+           (long long)nnz, K);
+    CK(hipGraphExecDestroy(exec));
+    CK(hipGraphDestroy(graph));
+    CL(lgcn_sched_destroy(sc));
+    return bad ? 1 : 0;
+}

@@ -42,7 +42,8 @@ def main():
             ("backward_bpr", lambda: engine.propagate_backward(g, Gs, K))]
     if os.environ.get("FWD_ONLY"):  # A/B timing: median of REPS forwards (and BPR backwards)
         reps = int(os.environ.get("REPS", "10"))
-        for name, fn in (runs[0], runs[2]):
+        sel = (runs[0], runs[1], runs[2]) if os.environ.get("DENSE") else (runs[0], runs[2])
+        for name, fn in sel:
             for _ in range(3):
                 fn()
             ts = []
@@ -54,7 +55,7 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(a.elapsed_time(b))
             print(f"{name}: median {np.median(ts):.3f} ms min {min(ts):.3f} "
-                  f"[{os.environ.get('LGCN_LIB', 'product')} slots={os.environ.get('LGCN_EMU_SLOTS', '')}]"
+                  f"[{os.environ.get('LGCN_LIB', 'product')}]"
                   f" all {' '.join(f'{t:.2f}' for t in ts)}", flush=True)
         return
     for name, fn in runs:
