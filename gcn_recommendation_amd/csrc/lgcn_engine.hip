@@ -661,19 +661,14 @@ int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host) {
     return 0;
 }
 
-int lgcn_stream_create_dedicated(void** stream) {
+int lgcn_stream_create(int32_t high, void** stream) {
     if (!stream) return LGCN_EINVAL;
-    int dev = 0, n_cu = 0;
-    if (hipError_t e = hipGetDevice(&dev)) return (int)e;
-    if (hipError_t e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev))
-        return (int)e;
-    if (n_cu < 1 || n_cu > 1024) return LGCN_EINVAL;
-    uint32_t mask[32];
-    const int words = (n_cu + 31) / 32;
-    for (int i = 0; i < words; ++i) mask[i] = 0xffffffffu;
-    if (n_cu % 32) mask[words - 1] = (1u << (n_cu % 32)) - 1u;
+    int least = 0, greatest = 0;
+    if (hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest)) return (int)e;
     hipStream_t s = nullptr;
-    if (hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask)) return (int)e;
+    if (hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking,
+                                                   high ? greatest : least))
+        return (int)e;
     *stream = s;
     return 0;
 }

@@ -80,12 +80,27 @@ def _equal_cost_bounds(cum, lo, hi, k):
     return np.maximum.accumulate(np.clip(b, lo, hi))
 
 
-def balanced_row_bounds(deg, world, row_cost=4.0, walk_deg=None, walk_factor=WALK_FACTOR):
+def balanced_row_bounds(deg, world, row_cost=4.0, walk_deg=None, walk_factor=WALK_FACTOR,
+                        max_rows_factor=1.25):
     """Contiguous row blocks of near-equal cost (row_costs: nnz + row_cost per row, walked rows
     at walk_factor x nnz): P+1 boundaries. A row costing more than a rank's share (a walked hub
     row) gets a rank of its own when the ranks allow it, and the rows between such rows share the
     other ranks in proportion to their cost — so the rank that owns the 2.77M-edge row carries no
-    other rows (rowpart balanced by walk cost)."""
+    other rows (rowpart balanced by walk cost). The exchange buffer is padded to the
+    largest block (n_max rows per rank), so with walk costs the per-row cost doubles until no
+    block holds more than max_rows_factor x N/P rows."""
+    n = len(deg)
+    b = _balanced_row_bounds(deg, world, row_cost, walk_deg, walk_factor)
+    for _ in range(12):
+        if walk_deg is None or world <= 1 or n == 0 or \
+                np.diff(b).max() <= max_rows_factor * n / world:
+            break
+        row_cost *= 2.0
+        b = _balanced_row_bounds(deg, world, row_cost, walk_deg, walk_factor)
+    return b
+
+
+def _balanced_row_bounds(deg, world, row_cost, walk_deg, walk_factor):
     cost = row_costs(deg, row_cost, walk_deg, walk_factor)
     n = cost.size
     if world <= 1 or n == 0:

@@ -163,7 +163,7 @@ ABI = [
     ("lgcn_error_string", ctypes.c_char_p, [ctypes.c_int]),
     ("lgcn_tune", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("lgcn_device_info", ctypes.c_int, [ctypes.c_int, _P, _P]),
-    ("lgcn_stream_create_dedicated", ctypes.c_int, [_P]),
+    ("lgcn_stream_create", ctypes.c_int, [_I32, _P]),
     ("lgcn_stream_destroy", ctypes.c_int, [_P]),
     ("lgcn_coo_inspect", ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
     ("lgcn_coo_to_csr", ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P]),
@@ -980,24 +980,22 @@ def _check_emb(segments, d, device):
 _scheds = {}
 
 
-def _side_stream(device, i=0, high=False, dedicated=False):
+def _side_stream(device, i=0, high=False):
     """Per-device side streams the emulated and chain rows run on beside the layer kernel
     (lgcn_sched), one per (index, priority); high = created at high priority, so their waves are
-    dispatched first; dedicated = normal priority on a hardware queue of its own
-    (lgcn_stream_create_dedicated, wrapped as a torch.cuda.ExternalStream)."""
+    dispatched first. Created by the library (lgcn_stream_create) and wrapped as
+    torch.cuda.ExternalStream: torch.cuda.Stream() hands out streams from a round-robin pool of
+    32 per priority, so a pooled side stream could be the very stream some caller (or a graph
+    capture) is using."""
     sc = _scheds.setdefault(("streams", str(device)), {})
-    key = (i, high, dedicated)
-    if key not in sc:
-        if dedicated:
-            lib = load_library()
-            h = ctypes.c_void_p()
-            with torch.cuda.device(device):
-                _check(lib.lgcn_stream_create_dedicated(ctypes.byref(h)),
-                       "lgcn_stream_create_dedicated")
-            sc[key] = torch.cuda.ExternalStream(h.value, device=device)
-        else:
-            sc[key] = torch.cuda.Stream(device, priority=-1 if high else 0)
-    return sc[key]
+    if (i, high) not in sc:
+        lib = load_library()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _check(lib.lgcn_stream_create(1 if high else 0, ctypes.byref(h)),
+                   "lgcn_stream_create")
+        sc[(i, high)] = torch.cuda.ExternalStream(h.value, device=device)
+    return sc[(i, high)]
 
 
 def _stream_priorities(n_aux, role="forward"):
@@ -1042,11 +1040,7 @@ class Sched:
     def __init__(self, device, n_aux, role="forward"):
         lib = load_library()
         self.lib, self.device, self.n_aux = lib, device, n_aux
-        # the backward's lane 1 at normal priority: streams with queues of their own, so the
-        # two lanes' 8 normal-priority streams do not take turns on HIP's 4 shared queues
-        ded = role == "backward" and n_aux >= 4 and \
-            os.environ.get("LGCN_DEDICATED_Q", "0") == "1"
-        self.streams = [_side_stream(device, i, hi, ded and i >= 3)
+        self.streams = [_side_stream(device, i, hi)
                         for i, hi in enumerate(_stream_priorities(n_aux, role))]
         arr = (ctypes.c_void_p * n_aux)(*[st.cuda_stream for st in self.streams])
         h = ctypes.c_void_p()
@@ -1084,8 +1078,7 @@ def sched_for(device, n_aux=None, role="forward"):
         return None
     # role "backward": lane 1 at normal priority on four streams of its own (_backward_role)
     key = (str(device), n_aux or n_aux_streams(), chain_enabled(),
-           os.environ.get("LGCN_SCHED_CLASSES", ""), os.environ.get("LGCN_DEDICATED_Q", ""),
-           role)
+           os.environ.get("LGCN_SCHED_CLASSES", ""), role)
     if key not in _scheds:
         _scheds[key] = Sched(device, key[1], role)
     return _scheds[key]

@@ -257,12 +257,11 @@ int lgcn_tune(int knob, int value);
 /* device properties the host side needs (CU count); returns 0/hipError */
 int lgcn_device_info(int device, int32_t* n_cu_host, int32_t* arch_major_host);
 
-/* A normal-priority stream with a hardware queue of its own on the current device: HIP serves
- * streams from a pool of GPU_MAX_HW_QUEUES queues per priority (default 4), and two streams on
- * one queue run in order — a schedule with more than four normal-priority streams (the
- * backward's two lanes at normal priority: 8) serialises on the shared queues. A stream created
- * with a CU mask always gets a new queue; every CU is enabled (no placement restriction). */
-int lgcn_stream_create_dedicated(void** stream);
+/* A stream of the schedule's own on the current device (non-blocking; high != 0: the greatest
+ * priority, else the least): the schedule's streams must be distinct from every stream the host
+ * hands out elsewhere — torch.cuda.Stream() returns streams from a round-robin pool of 32 per
+ * priority, so two of them can be one HIP stream. */
+int lgcn_stream_create(int32_t high, void** stream);
 int lgcn_stream_destroy(void* stream);
 
 /* ---- graph preparation (replaces the per-call COO handling inside torch.sparse.mm) ---------- */

@@ -133,7 +133,9 @@ def test_balanced_bounds_and_layout():
     deg[3_000] = 30_000   # below a rank's share by nnz, far above it as a walk
     for world in (4, 8):
         b0 = D.balanced_row_bounds(deg, world)
-        b1 = D.balanced_row_bounds(deg, world, walk_deg=20_000)
+        b1 = D.balanced_row_bounds(deg, world, walk_deg=20_000, max_rows_factor=2.0)
+        bc = D.balanced_row_bounds(deg, world, walk_deg=20_000)   # default row cap
+        assert np.diff(bc).max() <= 1.25 * deg.size / world
         assert len(b1) == world + 1 and b1[0] == 0 and b1[-1] == deg.size
         assert np.all(np.diff(b1) >= 1)
         own0 = np.searchsorted(b0, 3_000, side="right") - 1

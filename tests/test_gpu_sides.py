@@ -153,33 +153,22 @@ def test_classes_directed_operator(gpu_device, monkeypatch, brand_graph):
                           oracle.backward(r, c, v, G, 3).view(np.uint32))
 
 
-def test_dedicated_queue_streams_bitwise(gpu_device, monkeypatch, brand_graph):
-    """lgcn_stream_create_dedicated: the backward's lane 1 on normal-priority streams with queues
-    of their own (LGCN_DEDICATED_Q=1) — a working stream (torch work on it completes) and the
-    same bits as the oracle."""
-    from gcn_recommendation_amd import engine as E
-    lib = E.load_library()
-    h = __import__("ctypes").c_void_p()
-    with torch.cuda.device(gpu_device):
-        assert lib.lgcn_stream_create_dedicated(__import__("ctypes").byref(h)) == 0
-    st = torch.cuda.ExternalStream(h.value, device=gpu_device)
-    with torch.cuda.stream(st):
-        x = torch.arange(1 << 20, device=gpu_device, dtype=torch.float32).sum()
-    st.synchronize()
-    assert float(x) == float((1 << 20) * ((1 << 20) - 1) // 2)
-    assert lib.lgcn_stream_destroy(h) == 0
-    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
-    monkeypatch.setenv("LGCN_AUX_STREAMS", "7")
-    monkeypatch.setenv("LGCN_DEDICATED_Q", "1")
-    r, c, v, n = brand_graph
-    g = E.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
-    rng = np.random.default_rng(9)
-    G = _e0(rng, "xavier", n, 64)
-    G[rng.random(n) > 0.02] = 0.0
-    want = oracle.backward(r, c, v, G, 3)
-    for _ in range(3):   # the row-sparse schedule (role "backward") once the hint has landed
-        got = E.propagate_backward(g, _segs(G, gpu_device), 3, **KW).cpu().numpy()
-        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+def test_library_streams():
+    """lgcn_stream_create: the schedule's own streams (not torch's pooled ones) at both
+    priorities; torch work on them completes."""
+    import ctypes
+    lib = engine.load_library()
+    dev = torch.device("cuda:0")
+    for high in (0, 1):
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            assert lib.lgcn_stream_create(high, ctypes.byref(h)) == 0
+        st = torch.cuda.ExternalStream(h.value, device=dev)
+        with torch.cuda.stream(st):
+            x = torch.arange(1 << 20, device=dev, dtype=torch.float32).sum()
+        st.synchronize()
+        assert float(x) == float((1 << 20) * ((1 << 20) - 1) // 2)
+        assert lib.lgcn_stream_destroy(h) == 0
 
 
 def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):

@@ -1,6 +1,6 @@
 // C host (no torch, no Python in the process) capturing the library's own sided forward into a
 // HIP graph: the discriminating run for the capture crash of DESIGN §4d.
-// The graph (a bipartite user-item operator with walked item rows), the plans (the C planner:
+// The graph (a bipartite user-item-brand operator with walked item rows, brand hub rows), the plans (the C planner:
 // lgcn_plan_exact / lgcn_plan_scratch_bytes per segment) and the 7-stream
 // schedule are built as a C host builds them; then
 //   1. one eager lgcn_propagate_forward_sides (and _backward_sides) -> reference outputs;
@@ -69,9 +69,10 @@ static void* dev_alloc(size_t bytes) {
 int main(int argc, char** argv) {
     signal(SIGSEGV, on_segv);
     signal(SIGABRT, on_segv);
-    const int U = 60000, I = 4000, d = 64, K = argc > 1 ? atoi(argv[1]) : 3;
+    // users, items and brands (every item in one brand: brand rows of ~I/B items, side-0 hubs)
+    const int U = 60000, I = 4000, B = 20, d = 64, K = argc > 1 ? atoi(argv[1]) : 3;
     const int64_t n_inter = 300000;
-    const int n = U + I;
+    const int n = U + I + B;
     // -- the graph: Zipf item popularity, symmetric normalised adjacency (main.py:282-336 shape)
     std::mt19937_64 rng(5);
     std::vector<double> cdf(I);
@@ -90,14 +91,21 @@ int main(int argc, char** argv) {
         adj[e.first].push_back(U + e.second);
         adj[U + e.second].push_back(e.first);
     }
+    for (int i = 0; i < I; ++i) {
+        const int b = U + I + (int)(rng() % B);
+        adj[U + i].push_back(b);
+        adj[b].push_back(U + i);
+    }
     for (auto& a : adj) std::sort(a.begin(), a.end());
-    // -- slot order: side 0 (users) then side 1 (items), each degree-descending, stable
-    std::vector<int32_t> row_ids(n);
-    std::iota(row_ids.begin(), row_ids.end(), 0);
+    // -- slot order: side 0 (users, brands) then side 1 (items), each degree-descending, stable
+    std::vector<int32_t> row_ids;
+    for (int r = 0; r < n; ++r)
+        if (r < U || r >= U + I) row_ids.push_back(r);
+    for (int r = U; r < U + I; ++r) row_ids.push_back(r);
     auto by_deg = [&](int32_t a, int32_t b) { return adj[a].size() > adj[b].size(); };
-    std::stable_sort(row_ids.begin(), row_ids.begin() + U, by_deg);
-    std::stable_sort(row_ids.begin() + U, row_ids.end(), by_deg);
-    const int split = U;
+    const int split = U + B;
+    std::stable_sort(row_ids.begin(), row_ids.begin() + split, by_deg);
+    std::stable_sort(row_ids.begin() + split, row_ids.end(), by_deg);
     std::vector<int32_t> rowptr(n + 1, 0);
     std::vector<lgcn_edge_t> edges;
     for (int s = 0; s < n; ++s) {
@@ -163,7 +171,7 @@ int main(int argc, char** argv) {
     std::normal_distribution<float> nd(0.f, 0.1f);
     for (auto& x : e0) x = nd(rng);
     float* d_e0 = dev_copy(e0);
-    lgcn_rows_t emb = {d_e0, d_e0 + (size_t)U * d, d_e0 + (size_t)U * d, U, n, d};
+    lgcn_rows_t emb = {d_e0, d_e0 + (size_t)U * d, d_e0 + (size_t)(U + I) * d, U, U + I, d};
     std::vector<float*> layers(std::max(K - 1, 1));
     for (auto& l : layers) l = (float*)dev_alloc((size_t)n * d * 4);
     float* d_out = (float*)dev_alloc((size_t)n * d * 4);
