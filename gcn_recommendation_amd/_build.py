@@ -69,6 +69,24 @@ def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
     return out
 
 
+def build_capture_host(verbose=False):
+    """tools/capture_host: the C host that captures the library's two-lane schedule into a HIP
+    graph (tests/test_gpu_sides.py::test_c_host_captures_full_schedule), linked against the
+    in-tree liblgcn_engine.so (rpath $ORIGIN/../gcn_recommendation_amd)."""
+    src = os.path.join(ROOT, "tools", "capture_host.cpp")
+    exe = os.path.join(ROOT, "tools", "capture_host")
+    if os.path.exists(exe) and all(os.path.getmtime(exe) > os.path.getmtime(p)
+                                   for p in (src, OUT, HDRS[0])):
+        return exe
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O2", "-I", os.path.join(ROOT, "include"), src,
+           "-L", _PKG, "-llgcn_engine", "-Wl,-rpath,$ORIGIN/../gcn_recommendation_amd",
+           "-o", exe]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return exe
+
+
 if __name__ == "__main__":
     # python -m gcn_recommendation_amd._build [variant DEFINE=VALUE ...]
     import sys

@@ -1057,7 +1057,7 @@ struct EventPool {
     hipEvent_t ev[kPoolEvents];
     int n = 0;
     int next = 0;
-    int32_t state[4] = {0, 0, 0, 0};  // the latest call's schedule (lgcn_sched_state)
+    int32_t state[5] = {0, 0, 0, 0, 0};  // the latest call's schedule (lgcn_sched_state)
 };
 }  // namespace
 
@@ -1394,26 +1394,35 @@ bool capturing(hipStream_t s) {
 
 // The two lanes: lane 1 on its own streams when the schedule has them, else both lanes share
 // the caller's stream (half-layers then run in layer order, each still overlapped inside).
-// While `s` is being captured, lane 1 runs its half-layers on its main stream alone: a capture
-// that forks lane 1's own aux streams crashes hipStreamEndCapture on ROCm 7.2.0 with PyTorch
-// 2.10.0+rocm7.0 (this image's HIP runtime; rounds 3-5,
-// with every record on its own event too, while a plain-HIP replay of the same
-// stream/event sequence captures fine). The diagnostic build LGCN_CAPTURE_AUX_EXP keeps them.
-#ifdef LGCN_CAPTURE_AUX_EXP
-constexpr bool kCaptureAux = true;
-#else
-constexpr bool kCaptureAux = false;
-#endif
+// Captures: HIP runtimes before 7.2 segfault in hipStreamEndCapture on the full schedule — lane
+// 1's aux streams forked from its main stream and joined back, deferred parts, cross-lane waits
+// on aux streams (round 6, DESIGN §4e: the same C host binary captures, instantiates and replays
+// it bitwise on /opt/rocm's 7.2 runtime and crashes on the 7.0 runtime that the torch 2.10.0
+// +rocm7.0 wheel bundles, which is the one a torch process loads). Under a capture on such a
+// runtime lane 1 runs its half-layers on its main stream alone and the parts are joined every
+// half-layer; from 7.2 on a capture records the eager schedule itself.
+bool runtime_captures_full() {
+    static const bool ok = [] {
+        int v = 0;
+        return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
+    }();
+    return ok;
+}
+
+// the capture restrictions above apply to this call: `s` is being captured on an older runtime
+bool capture_restricted(hipStream_t s) { return capturing(s) && !runtime_captures_full(); }
+
 bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2], bool& l1_aux) {
     lanes[0] = Lane{s, sc};
     const bool two = sc && sc->lane1;
     const bool cap = capturing(s);
-    l1_aux = two && sc->lane1->n_aux > 0 && (!cap || kCaptureAux);
+    l1_aux = two && sc->lane1->n_aux > 0 && !(cap && !runtime_captures_full());
     lanes[1] = two ? Lane{sc->lane1_main, l1_aux ? sc->lane1 : nullptr} : lanes[0];
     if (sc) {
         sc->pool->state[0] = two ? 2 : 1;
         sc->pool->state[1] = l1_aux ? sc->lane1->n_aux : 0;
         sc->pool->state[2] = cap ? 1 : 0;
+        sc->pool->state[4] = cap && runtime_captures_full() ? 1 : 0;
     }
     return two;
 }
@@ -1554,11 +1563,11 @@ int run_sides(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* ro
     bool l1_aux = false;
     if (sched) sched->pool->next = 0;
     const bool two = make_lanes(sched, s, lanes, l1_aux);
-    // Under a HIP-graph capture the parts are joined into their lane at the end of every
-    // half-layer (no deferred parts, no early starts, no cross-lane waits on an aux stream): a
-    // capture with those crashed hipStreamEndCapture on this ROCm (round 5, in the first test
-    // that captured them); the captured graph keeps the per-class launches and the two lanes.
-    const bool cap = capturing(s);
+    // Under a HIP-graph capture on a runtime before 7.2 the parts are joined into their lane at
+    // the end of every half-layer (no deferred parts, no early starts, no cross-lane waits on an
+    // aux stream: runtime_captures_full); the captured graph keeps the per-class launches and
+    // the two lanes.
+    const bool cap = capture_restricted(s);
     const bool classes = sched && sched->classes && classes_hold(sd, plans) && !cap;
     if (sched) sched->pool->state[3] = classes ? 1 : 0;
     const int32_t lo[kSegs] = {0, sd.class_end[0], sd.class_end[1], sd.split};
@@ -1724,8 +1733,11 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
     }
 }
 
+int lgcn_capture_full_schedule(void) { return runtime_captures_full() ? 1 : 0; }
+
 int64_t lgcn_sched_state(const lgcn_sched_t* sc, int32_t what) {
-    if (!sc || what < LGCN_SCHED_STATE_LANES || what > LGCN_SCHED_STATE_CLASSES) return LGCN_EINVAL;
+    if (!sc || what < LGCN_SCHED_STATE_LANES || what > LGCN_SCHED_STATE_CAPTURE_FULL)
+        return LGCN_EINVAL;
     return sc->pool->state[what - LGCN_SCHED_STATE_LANES];
 }
 

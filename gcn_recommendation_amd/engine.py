@@ -31,6 +31,7 @@ SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
 SCHED_CLASSES = 16
 SCHED_LK_NORMAL = 17
 SCHED_STATE_LANES, SCHED_STATE_L1_AUX, SCHED_STATE_CAPTURING, SCHED_STATE_CLASSES = 1, 2, 3, 4
+SCHED_STATE_CAPTURE_FULL = 5
 # segments of a sided propagation: the three side-0 classes, then side 1
 N_SEGS = 4
 # phases of one exact layer recorded under SCHED_TRACE (lgcn.h)
@@ -164,6 +165,7 @@ ABI = [
     ("lgcn_tune", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("lgcn_device_info", ctypes.c_int, [ctypes.c_int, _P, _P]),
     ("lgcn_stream_create", ctypes.c_int, [_I32, _P]),
+    ("lgcn_capture_full_schedule", ctypes.c_int, []),
     ("lgcn_stream_destroy", ctypes.c_int, [_P]),
     ("lgcn_coo_inspect", ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
     ("lgcn_coo_to_csr", ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P]),
@@ -1236,6 +1238,7 @@ def _note_schedule(sc, graph):
                      "lanes": sc.state(SCHED_STATE_LANES),
                      "lane1_aux": sc.state(SCHED_STATE_L1_AUX),
                      "captured": bool(sc.state(SCHED_STATE_CAPTURING)),
+                     "capture_full": bool(sc.state(SCHED_STATE_CAPTURE_FULL)),
                      "classes": bool(sc.state(SCHED_STATE_CLASSES))}
 
 

@@ -517,13 +517,20 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        1's last) runs on aux_streams[2] at normal priority, so the
                                        side-0 mean overlaps it instead of waiting for its grid;
                                        0: on lane 1's main stream (same bits) */
-/* (under a HIP-graph capture lane 1 runs its half-layers on its main stream alone: DESIGN §4d) */
+/* Captures: a HIP runtime before 7.2 segfaults in hipStreamEndCapture on the full two-lane
+ * schedule (the same C host captures it on 7.2 and crashes on the 7.0 runtime the
+ * torch 2.10.0+rocm7.0 wheel bundles). Under a capture on such a runtime lane 1 runs its
+ * half-layers on its main stream alone and every part is joined at the end of its half-layer
+ * (same bits); from 7.2 on the capture records the eager schedule. 1 = this process's runtime
+ * captures the full schedule. */
+int lgcn_capture_full_schedule(void);
 int lgcn_sched_set(lgcn_sched_t* sched, int32_t knob, int64_t value);
 /* What the latest lgcn_propagate_*_sides call on this schedule ran (diagnostics, tests). */
 #define LGCN_SCHED_STATE_LANES     1  /* 2: two lanes, 1: one */
 #define LGCN_SCHED_STATE_L1_AUX    2  /* aux streams lane 1 ran its parts on (0: its main stream) */
 #define LGCN_SCHED_STATE_CAPTURING 3  /* 1: the caller's stream was being captured */
 #define LGCN_SCHED_STATE_CLASSES   4  /* 1: the class dependencies were used */
+#define LGCN_SCHED_STATE_CAPTURE_FULL 5  /* 1: captured with the eager schedule itself (below) */
 int64_t lgcn_sched_state(const lgcn_sched_t* sched, int32_t what);
 
 /* One whole layer under a hub plan: lgcn_spmm_layer (bundles, chunks and whole long rows) +

@@ -171,6 +171,23 @@ def test_library_streams():
         assert lib.lgcn_stream_destroy(h) == 0
 
 
+def test_c_host_captures_full_schedule():
+    """tools/capture_host.cpp (built by __graft_entry__.build() against liblgcn_engine.so; no torch
+    in its process, /opt/rocm's HIP runtime): the two-lane forward and backward with lane 1's own
+    aux streams, captured, instantiated and replayed bitwise equal to the eager calls."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                       "capture_host")
+    if not os.path.exists(exe):
+        pytest.skip("tools/capture_host not built (__graft_entry__.build())")
+    env = {k: v for k, v in os.environ.items() if k != "LD_LIBRARY_PATH"}
+    out = subprocess.run([exe, "3", "both"], capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "lane-1 aux streams under the capture 3" in out.stdout, out.stdout
+    assert "replays bitwise equal to eager" in out.stdout, out.stdout
+
+
 def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):
     """The model's entry (propagate_blocks: sides from the segment sizes) forward + autograd
     backward, and the forward captured in a HIP graph on the two lanes (the caller's stream, its
@@ -194,10 +211,12 @@ def test_sides_autograd_and_capture(gpu_device, monkeypatch, brand_graph):
     assert np.array_equal(got_b, oracle.backward(r, c, v, G, 3))
     x = [t.detach() for t in w]
     cap = engine.CapturedForward(g, x, 3, hub_threshold=128)
-    # the capture ran the two lanes (lane 1 without its own aux streams: the library's default
-    # under a capture: DESIGN §4d)
+    # the capture ran the two lanes; lane 1 keeps its own aux streams only on a HIP runtime that
+    # captures the full schedule (>= 7.2; the torch wheel's 7.0 does not: DESIGN §4e)
+    full = bool(engine.load_library().lgcn_capture_full_schedule())
     s = engine.last_schedule
-    assert (s["lanes"], s["lane1_aux"], s["captured"], s["aux_streams"]) == (2, 0, True, 7)
+    assert (s["lanes"], s["lane1_aux"], s["captured"], s["aux_streams"], s["capture_full"]) == \
+        (2, 3 if full else 0, True, 7, full)
     for _ in range(2):
         assert np.array_equal(cap.replay().cpu().numpy(), want)
 

@@ -7,10 +7,13 @@
 //   2. the same calls between hipStreamBeginCapture / hipStreamEndCapture on the caller's
 //      stream, hipGraphInstantiate, two hipGraphLaunch-es over NaN-filled outputs;
 //   3. the replays compared bitwise with the eager outputs; lgcn_sched_state reports how many
-//      aux streams lane 1 ran on under the capture (3 with the LGCN_CAPTURE_AUX_EXP library).
-// A SIGSEGV prints the native backtrace (execinfo) before the process dies.
-//   hipcc --offload-arch=gfx950 -O2 -I include tools/capture_host.cpp \
-//     -L <dir> -l<lgcn_engine | lgcn_capaux> -Wl,-rpath,<dir> -o tools/capture_host
+//      aux streams lane 1 ran on under the capture (3 on a HIP runtime >= 7.2, which captures
+//      the full schedule: lgcn_capture_full_schedule).
+// A SIGSEGV prints the native backtrace (execinfo) before the process dies. Built by
+// __graft_entry__.build() (gcn_recommendation_amd/_build.py build_capture_host); run by
+// tests/test_gpu_sides.py::test_c_host_captures_full_schedule. DESIGN §4e: on the 7.0 HIP runtime
+// the torch wheel bundles (LD_LIBRARY_PATH to a libamdhip64.so.7 link into torch/lib) the full
+// schedule's capture segfaults in hipStreamEndCapture; on /opt/rocm's 7.2 it replays bitwise.
 #include <execinfo.h>
 #include <hip/hip_runtime.h>
 #include <signal.h>

@@ -1,8 +1,12 @@
-"""The torch side of the capture investigation: engine.CapturedForward of the
-sided forward over the brand graph of tests/test_gpu_sides.py, in a fresh process, with the
-library given by LGCN_LIB (the LGCN_CAPTURE_AUX_EXP build keeps lane 1's aux streams under the
-capture). Prints the schedule the capture ran and whether two replays are bitwise equal to the
-oracle. A crash here with tools/capture_host.cpp passing isolates torch's capture path."""
+"""The torch side of the round-6 capture investigation: the sided forward over the
+brand graph of tests/test_gpu_sides.py captured under torch.cuda.graph in a fresh process —
+engine.CapturedForward, the same with capture_error_mode="relaxed", or the bare library call
+with every buffer allocated before the capture (argv[1]: engine | relaxed | prealloc). With the
+full schedule under the capture (the investigation's LGCN_CAPTURE_AUX_EXP build) every mode
+segfaulted in hipStreamEndCapture — the torch process runs the 7.0 HIP runtime of the torch wheel,
+and tools/capture_host.cpp crashes the same way on it. The library now restricts a capture on
+runtimes before 7.2 (lgcn_capture_full_schedule), so this probe replays bitwise with lane 1 on its
+main stream."""
 import os
 import sys
 

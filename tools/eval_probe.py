@@ -36,8 +36,12 @@ def main():
     mu = np.repeat(users, 3)
     mi = rng.integers(0, args.items, mu.size)
     mrow, mit = E.mask_csr(mu, mi, U)
-    E.topk_fused(ue, ie, users, mrow, mit, 20)
+    res = E.topk_fused(ue, ie, users, mrow, mit, 20)
     torch.cuda.synchronize()
+    import hashlib
+    h = hashlib.sha1()
+    for t in (res if isinstance(res, (tuple, list)) else [res]):
+        h.update(t.cpu().numpy().tobytes() if hasattr(t, "cpu") else np.asarray(t).tobytes())
     t0 = time.time()
     for _ in range(args.reps):
         E.topk_fused(ue, ie, users, mrow, mit, 20)
@@ -45,7 +49,8 @@ def main():
     ms = (time.time() - t0) / args.reps * 1e3
     flops = 2.0 * args.users * args.items * args.d
     print(json.dumps({"d": args.d, "users": args.users, "items": args.items, "ms": round(ms, 2),
-                      "tflops": round(flops / (ms / 1e3) / 1e12, 1)}), flush=True)
+                      "tflops": round(flops / (ms / 1e3) / 1e12, 1), "sha": h.hexdigest()[:16],
+                      "lib": os.environ.get("LGCN_LIB", "product")}), flush=True)
 
 
 if __name__ == "__main__":

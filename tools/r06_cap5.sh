@@ -4,6 +4,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 bash tools/trace_fwd.sh r06 || exit 1
+for rep in 1 2; do for L in "" gcn_recommendation_amd/_variants/liblgcn_evthr.so; do
+  LGCN_LIB=$L timeout -k 10 180 python -u tools/eval_probe.py --reps 5 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/eval_ab.log || exit 1
+done; done
 TL=$(python -c "import torch, os; print(os.path.join(os.path.dirname(torch.__file__), 'lib'))")
 mkdir -p /tmp/hip70 && ln -sf $TL/libamdhip64.so /tmp/hip70/libamdhip64.so.7
 echo "torch HIP runtime: $TL/libamdhip64.so"
