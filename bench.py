@@ -832,6 +832,19 @@ def main():
     e.record()
     torch.cuda.synchronize()
     bwd_ms = a.elapsed_time(e) / args.steps
+    # the same dense G with the row mask forced (round 5's default: every row live, the masked and
+    # live-edge kernels run anyway) and with the mask off (the dense kernels, as the auto mode now
+    # picks from the hint ring): the round-5 16.4 vs 13.1 ms question answered on one G
+    forced = {}
+    for mode in ("on", "off"):
+        engine.propagate_backward(g, gsegs, K, hub_thr, sparse=mode)
+        torch.cuda.synchronize()
+        a.record()
+        for _ in range(args.steps):
+            engine.propagate_backward(g, gsegs, K, hub_thr, sparse=mode)
+        e.record()
+        torch.cuda.synchronize()
+        forced[mode] = round(a.elapsed_time(e) / args.steps, 4)
     # the upstream gradient of one BPR batch (main.py:496-497: 2048 users, 2048 pos + 2048 neg
     # items): row-sparse, so the masked backward gathers only its live rows in layer 1
     rs = np.random.default_rng(1)
@@ -839,9 +852,9 @@ def main():
         t.zero_()
     gsegs[0][torch.from_numpy(rs.integers(0, U, 2048)).to(dev)] = 1e-3
     gsegs[1][torch.from_numpy(rs.integers(0, I, 4096)).to(dev)] = -1e-3
-    for _ in range(2):
+    for _ in range(3):   # (the first call still follows the dense G's hint)
         engine.propagate_backward(g, gsegs, K, hub_thr)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     a.record()
     for _ in range(args.steps):
         engine.propagate_backward(g, gsegs, K, hub_thr)
@@ -851,7 +864,10 @@ def main():
     result["backward"] = {"ms_per_step": round(bwd_ms, 4),
                           "propagated_edges_per_s": round(K * nnz / (bwd_ms / 1e3), 1),
                           "what": "dE0 = sum_k (Â^T)^k G/(K+1), Horner order, G read in place "
-                                  "(dense G)",
+                                  "(dense G; auto mode: no row mask once the hint ring says G is "
+                                  "dense)",
+                          "dense_G_mask_forced_ms": forced["on"],
+                          "dense_G_mask_off_ms": forced["off"],
                           "bpr_batch_G_ms_per_step": round(bpr_ms, 4),
                           "bpr_batch_G": "G = a BPR batch's output gradient (<= 6144 live rows): "
                                          "row-sparse path (lgcn_rows_nonzero mask)"}

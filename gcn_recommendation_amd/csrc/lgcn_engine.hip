@@ -1077,6 +1077,10 @@ struct lgcn_sched {
     hipEvent_t* timing_sides;  // optional [8 K] (LGCN_SCHED_TIMING_SIDES)
     int classes;               // LGCN_SCHED_CLASSES (default 1)
     int lk_normal;             // LGCN_SCHED_LK_NORMAL (default 1)
+    // LGCN_SCHED_LANE1_SHARED: lane 1 on the caller's stream and lane 0's aux streams in reverse
+    // order (lane1s: that view), so each of lane 1's streams is one of lane 0's
+    int lane1_shared;
+    lgcn_sched* lane1s;
 };
 
 namespace {
@@ -1414,13 +1418,15 @@ bool capture_restricted(hipStream_t s) { return capturing(s) && !runtime_capture
 
 bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2], bool& l1_aux) {
     lanes[0] = Lane{s, sc};
-    const bool two = sc && sc->lane1;
+    const bool shared = sc && sc->lane1_shared && sc->lane1s;
+    const bool two = sc && (sc->lane1 || shared);
+    const lgcn_sched* l1v = shared ? sc->lane1s : (sc ? sc->lane1 : nullptr);
     const bool cap = capturing(s);
-    l1_aux = two && sc->lane1->n_aux > 0 && !(cap && !runtime_captures_full());
-    lanes[1] = two ? Lane{sc->lane1_main, l1_aux ? sc->lane1 : nullptr} : lanes[0];
+    l1_aux = two && l1v->n_aux > 0 && !(cap && !runtime_captures_full());
+    lanes[1] = two ? Lane{shared ? s : sc->lane1_main, l1_aux ? l1v : nullptr} : lanes[0];
     if (sc) {
         sc->pool->state[0] = two ? 2 : 1;
-        sc->pool->state[1] = l1_aux ? sc->lane1->n_aux : 0;
+        sc->pool->state[1] = l1_aux ? l1v->n_aux : 0;
         sc->pool->state[2] = cap ? 1 : 0;
         sc->pool->state[4] = cap && runtime_captures_full() ? 1 : 0;
     }
@@ -1428,25 +1434,23 @@ bool make_lanes(const lgcn_sched* sc, hipStream_t s, Lane lanes[2], bool& l1_aux
 }
 
 // Lane 1 forked from the caller's stream: its main stream and its aux streams wait on `s`.
-int fork_lanes(const lgcn_sched* sc, bool two, bool l1_aux, hipStream_t s) {
+int fork_lanes(const lgcn_sched* sc, bool two, const Lane& l1, hipStream_t s) {
     if (!two) return 0;
     hipEvent_t f;
     if (int e = record(sc, s, &f)) return e;
-    if (int e = wait_ev(sc->lane1_main, f)) return e;
-    const lgcn_sched* l1 = sc->lane1;
-    for (int i = 0; i < (l1_aux ? l1->n_aux : 0); ++i)
-        if (int e = wait_ev(l1->aux[i], f)) return e;
+    if (int e = wait_ev(l1.main, f)) return e;
+    for (int i = 0; i < (l1.view ? l1.view->n_aux : 0); ++i)
+        if (int e = wait_ev(l1.view->aux[i], f)) return e;
     return 0;
 }
 
 // Lane 1 back into the caller's stream: its main stream and its aux streams, each joined into
 // `s` directly.
-int join_lanes(const lgcn_sched* sc, bool two, bool l1_aux, hipStream_t s) {
+int join_lanes(const lgcn_sched* sc, bool two, const Lane& l1, hipStream_t s) {
     if (!two) return 0;
-    if (int e = link(sc, sc->lane1_main, s)) return e;
-    const lgcn_sched* l1 = sc->lane1;
-    for (int i = 0; i < (l1_aux ? l1->n_aux : 0); ++i)
-        if (int e = link(sc, l1->aux[i], s)) return e;
+    if (int e = link(sc, l1.main, s)) return e;
+    for (int i = 0; i < (l1.view ? l1.view->n_aux : 0); ++i)
+        if (int e = link(sc, l1.view->aux[i], s)) return e;
     return 0;
 }
 
@@ -1574,7 +1578,7 @@ int run_sides(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* ro
     const int32_t hi[kSegs] = {sd.class_end[0], sd.class_end[1], sd.split, 0};
     auto seg_hi = [&](int g, int32_t n) { return g == 3 ? n : hi[g]; };
     const int32_t n = sd.n;
-    if (int e = fork_lanes(sched, two, l1_aux, s)) return e;  // lane 1 starts where `s` is
+    if (int e = fork_lanes(sched, two, lanes[1], s)) return e;  // lane 1 starts where `s` is
     constexpr int KM = LGCN_MAX_LAYERS + 2;
     hipEvent_t cls[KM][3] = {}, ab[KM] = {}, rest[KM] = {}, part[KM][2] = {};
     for (int k = 1; k <= K; ++k) {
@@ -1631,7 +1635,7 @@ int run_sides(const int32_t* rowptr, const lgcn_edge_t* edges, const int32_t* ro
             ab[k] = k == 1 ? cls[k][1] : cls[k][0];
         }
     }
-    return join_lanes(sched, two, l1_aux, s);
+    return join_lanes(sched, two, lanes[1], s);
 }
 }  // namespace
 
@@ -1660,6 +1664,19 @@ int lgcn_sched_create(void* const* aux_streams, int32_t n_aux, lgcn_sched_t** ou
     for (; pool->n < kPoolEvents && !e; ++pool->n)
         e = herr(hipEventCreateWithFlags(&pool->ev[pool->n], hipEventDisableTiming));
     if (e) --pool->n;  // (the failed slot holds no event)
+    if (!e) {
+        sc->lane1s = new (std::nothrow) lgcn_sched();
+        if (!sc->lane1s) e = LGCN_EINVAL;
+        if (!e) {
+            lgcn_sched* l1 = sc->lane1s;
+            memset(l1, 0, sizeof(*l1));
+            l1->pool = pool;
+            l1->n_aux = n0;
+            l1->chain = 1;
+            l1->classes = 1;
+            for (int i = 0; i < n0; ++i) l1->aux[i] = sc->aux[n0 - 1 - i];
+        }
+    }
     if (!e && n_aux >= 4) {
         sc->lane1_main = reinterpret_cast<hipStream_t>(aux_streams[3]);
         sc->lane1 = new (std::nothrow) lgcn_sched();
@@ -1689,7 +1706,8 @@ int lgcn_sched_destroy(lgcn_sched_t* sc) {
         for (int i = 0; i < sc->pool->n; ++i) (void)hipEventDestroy(sc->pool->ev[i]);
         delete sc->pool;
     }
-    delete sc->lane1;  // (a view: shares the root's pool)
+    delete sc->lane1;  // (views: share the root's pool)
+    delete sc->lane1s;
     delete sc;
     return 0;
 }
@@ -1702,10 +1720,15 @@ int lgcn_sched_set(lgcn_sched_t* sc, int32_t knob, int64_t value) {
             if (value < 0 || value > LGCN_EMU_MAX_WALK_SLOTS) return LGCN_EINVAL;
             sc->slots[knob - LGCN_SCHED_SLOTS0] = (int32_t)value;
             if (sc->lane1) sc->lane1->slots[knob - LGCN_SCHED_SLOTS0] = (int32_t)value;
+            if (sc->lane1s) sc->lane1s->slots[knob - LGCN_SCHED_SLOTS0] = (int32_t)value;
             return 0;
         case LGCN_SCHED_CHAIN:
             sc->chain = value != 0;
             if (sc->lane1) sc->lane1->chain = value != 0;
+            if (sc->lane1s) sc->lane1s->chain = value != 0;
+            return 0;
+        case LGCN_SCHED_LANE1_SHARED:
+            sc->lane1_shared = value != 0;
             return 0;
         case LGCN_SCHED_TIMING_START:
             sc->t0 = reinterpret_cast<hipEvent_t>(value);

@@ -30,6 +30,7 @@ SCHED_SLOTS0, SCHED_SLOTS1, SCHED_CHAIN, SCHED_TIMING_START, SCHED_TIMING_END, S
 SCHED_TRACE_SIDES, SCHED_TIMING_SIDES = 7, 8
 SCHED_CLASSES = 16
 SCHED_LK_NORMAL = 17
+SCHED_LANE1_SHARED = 18
 SCHED_STATE_LANES, SCHED_STATE_L1_AUX, SCHED_STATE_CAPTURING, SCHED_STATE_CLASSES = 1, 2, 3, 4
 SCHED_STATE_CAPTURE_FULL = 5
 # segments of a sided propagation: the three side-0 classes, then side 1
@@ -990,6 +991,14 @@ def _side_stream(device, i=0, high=False):
     32 per priority, so a pooled side stream could be the very stream some caller (or a graph
     capture) is using."""
     sc = _scheds.setdefault(("streams", str(device)), {})
+    if (i, high) not in sc and i >= 3 and not high:
+        # the row-sparse backward's lane 1 (role "backward"): four of torch's pooled
+        # normal-priority streams, as round 5 — HIP maps them onto the normal-priority hardware
+        # queues lane 0's streams hold, pairwise, which serialises the two lanes' half-layers in
+        # issue order: the fastest BPR-batch backward measured (DESIGN §4e: 8.4-9.3 ms against
+        # 9.4-9.5 with lane 0's streams shared outright and 11 ms with library-created streams,
+        # which HIP paired differently)
+        sc[(i, high)] = torch.cuda.Stream(device)
     if (i, high) not in sc:
         lib = load_library()
         h = ctypes.c_void_p()
@@ -1007,10 +1016,10 @@ def _stream_priorities(n_aux, role="forward"):
     Measured at C3 against: no priorities, lane 0's aux streams, both
     lanes' part-0 streams, lane 1's layer kernels or its chains at normal priority (with 8
     queues per priority) — none faster, most slower."""
+    if role == "backward":  # (sched_for: the backward's lanes share lane 0's normal streams)
+        return [False] * n_aux
     if n_aux <= 3:
         return [i == 0 for i in range(n_aux)]
-    if role == "backward":  # (sched_for: the backward's lanes both at normal priority)
-        return [False] * n_aux
     return [i >= 3 for i in range(n_aux)]
 
 
@@ -1039,7 +1048,7 @@ class Sched:
     """lgcn_sched_t over this device's side streams (created once per device and stream count;
     the C library owns the fork/join events). n_aux >= 4: two lanes (lgcn_propagate_*_sides)."""
 
-    def __init__(self, device, n_aux, role="forward"):
+    def __init__(self, device, n_aux, role="forward", lane1_shared=False):
         lib = load_library()
         self.lib, self.device, self.n_aux = lib, device, n_aux
         self.streams = [_side_stream(device, i, hi)
@@ -1056,6 +1065,8 @@ class Sched:
         # LGCN_SCHED_CLASSES=0: the walked parts of side 1 wait for the whole side-0 half-layer
         # (A/B; same bits)
         self.set(SCHED_CLASSES, 0 if os.environ.get("LGCN_SCHED_CLASSES", "1") == "0" else 1)
+        if lane1_shared:
+            self.set(SCHED_LANE1_SHARED, 1)
 
     def state(self, what):
         """lgcn_sched_state: what the latest sided call on this schedule ran."""
@@ -1075,14 +1086,17 @@ class Sched:
 def sched_for(device, n_aux=None, role="forward"):
     """The device's Sched (None with LGCN_EMU_OVERLAP=0: every part in order on the caller's
     stream). n_aux: default n_aux_streams(). Made outside any capture on first use (the C
-    library creates its events there; a captured call reuses them)."""
+    library creates its events there; a captured call reuses them).
+
+    role "backward" (a row-sparse G, _backward_role): both lanes at normal priority, lane 1 on
+    four of torch's pooled streams (_side_stream), which HIP pairs with lane 0's hardware queues
+    (DESIGN §4e)."""
     if not emu_overlap_enabled():
         return None
-    # role "backward": lane 1 at normal priority on four streams of its own (_backward_role)
-    key = (str(device), n_aux or n_aux_streams(), chain_enabled(),
-           os.environ.get("LGCN_SCHED_CLASSES", ""), role)
+    n = n_aux or n_aux_streams()
+    key = (str(device), n, chain_enabled(), os.environ.get("LGCN_SCHED_CLASSES", ""), role)
     if key not in _scheds:
-        _scheds[key] = Sched(device, key[1], role)
+        _scheds[key] = Sched(device, n, role)
     return _scheds[key]
 
 

@@ -517,6 +517,11 @@ int lgcn_sched_destroy(lgcn_sched_t* sched);
                                        1's last) runs on aux_streams[2] at normal priority, so the
                                        side-0 mean overlaps it instead of waiting for its grid;
                                        0: on lane 1's main stream (same bits) */
+#define LGCN_SCHED_LANE1_SHARED 18  /* 1: lgcn_propagate_*_sides runs lane 1 on the caller's stream
+                                       and aux_streams[2], [1], [0] (lane 0's, reversed): two lanes
+                                       of half-layers that share lane 0's streams — the schedule of
+                                       a row-sparse backward; the rest of aux_streams
+                                       is not used (same bits) */
 /* Captures: a HIP runtime before 7.2 segfaults in hipStreamEndCapture on the full two-lane
  * schedule (the same C host captures it on 7.2 and crashes on the 7.0 runtime the
  * torch 2.10.0+rocm7.0 wheel bundles). Under a capture on such a runtime lane 1 runs its

@@ -171,6 +171,27 @@ def test_library_streams():
         assert lib.lgcn_stream_destroy(h) == 0
 
 
+def test_lane1_shared_bitwise(gpu_device, monkeypatch, brand_graph):
+    """LGCN_SCHED_LANE1_SHARED: lane 1 on the caller's stream and lane 0's aux streams reversed
+    (two lanes of half-layers on three aux streams): forward and row-sparse / dense backward
+    bitwise."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    sc = engine.Sched(gpu_device, 3, "backward", lane1_shared=True)
+    monkeypatch.setattr(engine, "sched_for", lambda dev, n_aux=None, role="forward": sc)
+    r, c, v, n = brand_graph
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    rng = np.random.default_rng(12)
+    e0 = _e0(rng, "xavier", n, 64)
+    got = engine.propagate_forward(g, _segs(e0, gpu_device), 3, **KW).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), oracle.forward(r, c, v, e0, 3).view(np.uint32))
+    assert (engine.last_schedule["lanes"], engine.last_schedule["lane1_aux"]) == (2, 3)
+    G = _e0(rng, "xavier", n, 64)
+    for frac in (0.03, 1.0):
+        Gm = np.where(rng.random((n, 1)) < frac, G, 0.0).astype(np.float32)
+        got_b = engine.propagate_backward(g, _segs(Gm, gpu_device), 3, **KW).cpu().numpy()
+        assert np.array_equal(got_b.view(np.uint32), oracle.backward(r, c, v, Gm, 3).view(np.uint32))
+
+
 def test_c_host_captures_full_schedule():
     """tools/capture_host.cpp (built by __graft_entry__.build() against liblgcn_engine.so; no torch
     in its process, /opt/rocm's HIP runtime): the two-lane forward and backward with lane 1's own
