@@ -1366,7 +1366,8 @@ def _sparse_grad_mode():
     return m
 
 
-_live_hint = {}  # device -> [slots, events, scales, next slot, last role]: recent live-row counts
+_live_hint = {}  # device -> [slots, events, scales, next slot, last role, last dense]: recent
+#                 live-row counts
 _HINT_SLOTS = 8
 _HINT_SAMPLE = 64  # a dense-path call counts the live rows of every 64th row of G (an estimate)
 
@@ -1376,7 +1377,7 @@ def _hint_entry(dev):
     h = _live_hint.get(key)
     if h is None:
         h = [torch.empty(_HINT_SLOTS, dtype=torch.int32, pin_memory=True),
-             [None] * _HINT_SLOTS, [1] * _HINT_SLOTS, 0, "forward"]
+             [None] * _HINT_SLOTS, [1] * _HINT_SLOTS, 0, "forward", False]
         _live_hint[key] = h
     return h
 
@@ -1406,14 +1407,16 @@ def _hint_push(dev, cnt, scale=1):
 
 def _hint_dense(dev, n):
     """True when the newest landed count says G was dense (>= n/8 live rows) — the mask would
-    mark every row, so the backward skips it and runs the dense kernels (round 6: dense backward
-    16.4 -> see DESIGN §4e). False before any count has landed and under a capture."""
-    if os.environ.get("LGCN_DENSE_SKIP_MASK", "1") == "0":
-        return False
+    mark every row, so the backward skips it and runs the dense kernels. With no
+    count landed (the host more than the ring's 8 calls ahead of the device) the previous
+    decision stays; False before any count has landed and under a capture."""
     if torch.cuda.is_current_stream_capturing():
         return False
+    h = _hint_entry(dev)
     c = _hint_latest(dev)
-    return c is not None and c * 8 >= n
+    if c is not None:
+        h[5] = c * 8 >= n
+    return h[5]
 
 
 def _sampled_live_count(segs, d, dev):

@@ -23,7 +23,10 @@ from gcn_recommendation_amd import engine  # noqa: E402
 def main():
     cfg = bench.CONFIGS[os.environ.get("CFG", "c3")]
     dev = torch.device("cuda:0")
-    engine.load_library()
+    lib = engine.load_library()
+    for kv in filter(None, os.environ.get("TUNE", "").split(",")):  # A/B: lgcn_tune knob:value
+        k, val = (int(t) for t in kv.split(":"))
+        lib.lgcn_tune(k, val)
     r, c, v, _, _, _ = bench.make_graph(cfg, "powerlaw", 16)
     U, I = cfg["users"], cfg["items"]
     n, d, K = U + I, cfg["d"], cfg["K"]
@@ -55,7 +58,7 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(a.elapsed_time(b))
             print(f"{name}: median {np.median(ts):.3f} ms min {min(ts):.3f} "
-                  f"[{os.environ.get('LGCN_LIB', 'product')}]"
+                  f"[{os.environ.get('LGCN_LIB', 'product')} {os.environ.get('TUNE', '')}]"
                   f" all {' '.join(f'{t:.2f}' for t in ts)}", flush=True)
         return
     for name, fn in runs:
