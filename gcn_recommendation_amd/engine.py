@@ -1384,7 +1384,7 @@ def _hint_entry(dev):
 
 def _hint_latest(dev):
     """The newest landed live-row count of G (scaled up when sampled), or None."""
-    slots, evs, scales, nxt, _ = _hint_entry(dev)
+    slots, evs, scales, nxt = _hint_entry(dev)[:4]
     for k in range(1, _HINT_SLOTS + 1):   # newest first
         i = (nxt - k) % _HINT_SLOTS
         if evs[i] is not None and evs[i].query():
@@ -1395,7 +1395,7 @@ def _hint_latest(dev):
 def _hint_push(dev, cnt, scale=1):
     """Copy the device count `cnt` into the next pinned slot, asynchronously."""
     h = _hint_entry(dev)
-    slots, evs, scales, nxt, _ = h
+    slots, evs, scales, nxt = h[:4]
     slot = nxt % _HINT_SLOTS
     slots[slot:slot + 1].copy_(cnt.view(-1)[:1], non_blocking=True)
     if evs[slot] is None:

@@ -171,6 +171,26 @@ def test_library_streams():
         assert lib.lgcn_stream_destroy(h) == 0
 
 
+def test_backward_hint_ring(gpu_device, monkeypatch, brand_graph):
+    """The backward's asynchronous live-row hints (engine._hint_*): 12 back-to-back calls (more
+    than the ring's 8 slots in flight) on a dense G end with the dense decision, on a BPR-like G
+    with the row-sparse one; every call bitwise either way."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    r, c, v, n = brand_graph
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    rng = np.random.default_rng(13)
+    G = _e0(rng, "xavier", n, 64)
+    Gs = np.where(rng.random((n, 1)) < 0.01, G, 0.0).astype(np.float32)
+    for Gx, dense in ((G, True), (Gs, False), (G, True)):
+        want = oracle.backward(r, c, v, Gx, 3)
+        segs = _segs(Gx, gpu_device)
+        outs = [engine.propagate_backward(g, segs, 3, **KW) for _ in range(12)]
+        torch.cuda.synchronize()
+        for o in outs:
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))
+        assert engine._hint_dense(gpu_device, n) is dense
+
+
 def test_lane1_shared_bitwise(gpu_device, monkeypatch, brand_graph):
     """LGCN_SCHED_LANE1_SHARED: lane 1 on the caller's stream and lane 0's aux streams reversed
     (two lanes of half-layers on three aux streams): forward and row-sparse / dense backward
