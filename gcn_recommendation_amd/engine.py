@@ -399,11 +399,11 @@ class HubPlan:
     def n_long(self):
         return self.n_items if self.mode == "exact" else 0
 
-    def walk_parts(self, nnz, backward=False):
+    def walk_parts(self, nnz, backward=False, part0=None):
         """(part_rows, part_blocks): the emulated rows cut into part 0 (rows of more than
-        LGCN_EMU_PART0 = 8192 blocks, the longest walks: the layer's critical path), part 1 (more
+        walk_cut_blocks' b0 blocks, the longest walks: the layer's critical path), part 1 (more
         than chain_max_degree blocks) and the chain rows (lgcn_hub_plan_t emu_part_*)."""
-        b0, b1 = walk_cut_blocks(nnz, backward)
+        b0, b1 = walk_cut_blocks(nnz, backward, part0)
         nb = self.emu_nb
         cum = np.concatenate([[0], np.cumsum(nb)])
         r0, r1 = int((nb > b0).sum()), int((nb > b1).sum())
@@ -453,7 +453,7 @@ class HubPlan:
             self._live = None
 
     def struct(self, d, device, nnz=None, walk_all=False, scratch_set=0, live=False,
-               backward=False):
+               backward=False, part0=None):
         """lgcn_hub_plan_t for width d. nnz: the operator's nonzeros (sets the chain/walk cut;
         None = every emulated row walked). walk_all: the chain rows are walked too (no chain
         kernel for this d / alignment, or LGCN_CHAIN=0), so the scratch covers every block.
@@ -463,7 +463,7 @@ class HubPlan:
             rows = [self.n_emu_rows, self.n_emu_rows] if nnz is None else None
             blocks = [self.n_emu_blocks, self.n_emu_blocks] if nnz is None else None
         if nnz is not None:
-            rows, blocks = self.walk_parts(nnz, backward)
+            rows, blocks = self.walk_parts(nnz, backward, part0)
         need = self.n_emu_blocks if (walk_all or nnz is None) else blocks[1]
         part, rel, meta, stage, eout = self.scratch(d, device, need, scratch_set)
         p = PlanT()
@@ -736,11 +736,23 @@ def classes_enabled():
     return os.environ.get("LGCN_CLASSES", "0") == "1"
 
 
-def walk_cut_blocks(nnz, backward=False):
-    """(b0, b1): the emulated rows of more than b0 blocks are part 0 (LGCN_EMU_PART0, 8192),
-    of more than b1 = chain cut / LGCN_EMU_BLOCK part 1 (walked); the rest run as chains."""
+# Part-0 cut of the row-sparse (BPR-batch) backward: its first layer runs live-edge chains, and
+# its later layers gain from walking more of the longest rows with part 0's many slots on their
+# own stream (C3, A/B on one box, interleaved twice: BPR backward 9.35 / 9.73 -> 8.81 / 9.30 ms
+# at 2048 blocks; the forward and the dense-G backward lose at 2048: 11.32 / 11.97 -> 11.71 /
+# 12.33 and 13.55 / 13.93 -> 15.80 / 14.39 ms, so they keep 8192; profiles/r06_ab_part0_slots.log).
+# Not with side-0 classes (LGCN_CLASSES=1): those were cut with the forward's part 0, and the
+# schedule's class waits name the parts by that cut.
+PART0_SPARSE_BACKWARD = 2048
+
+
+def walk_cut_blocks(nnz, backward=False, part0=None):
+    """(b0, b1): the emulated rows of more than b0 blocks are part 0 (LGCN_EMU_PART0, else
+    part0, else 8192), of more than b1 = chain cut / LGCN_EMU_BLOCK part 1 (walked); the rest
+    run as chains."""
     b1 = -(-chain_max_degree(nnz, backward) // LGCN_EMU_BLOCK)
-    return max(int(os.environ.get("LGCN_EMU_PART0", "8192")), b1), b1
+    b0 = int(os.environ.get("LGCN_EMU_PART0", "") or part0 or 8192)
+    return max(b0, b1), b1
 
 
 def side_classes(lib, g, stream):
@@ -1182,10 +1194,10 @@ def live_enabled():
 
 
 def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=False,
-                backward=False):
+                backward=False, part0=None):
     """The 8 lgcn_hub_plan_t of lgcn_propagate_*_sides: plans[2 * segment + set] (segments: the
     side-0 classes, side 1). live: attach the live-edge scratch (the backward of a row-sparse
-    G)."""
+    G). part0: the part-0 cut in blocks (walk_cut_blocks)."""
     lib = load_library()
     hps = graph.side_hubs(hub_threshold, mode=hub_mode, emu_min=emu_min)
     chains = chain_enabled() and bool(lib.lgcn_chain_supported(d)) and xs_aligned
@@ -1194,7 +1206,7 @@ def _side_plans(graph, d, hub_threshold, hub_mode, emu_min, xs_aligned, live=Fal
         for j in (0, 1):
             arr[2 * g + j] = hps[g].struct(d, graph.device, nnz=graph.nnz, walk_all=not chains,
                                            scratch_set=j, live=live and live_enabled(),
-                                           backward=backward)
+                                           backward=backward, part0=part0)
     return arr, hps
 
 
@@ -1493,9 +1505,12 @@ def propagate_backward(graph, grad_out, K, hub_threshold=None, sparse=None, hub_
                 nz, cnt = rows_nonzero(segs, d, dev)
         work = torch.empty((n, d), dtype=torch.float32, device=dev) if K > 1 else None
         if use_sides(gt):
+            role = _backward_role(dev, n, cnt, scale)
             plans, _ = _side_plans(gt, d, hub_threshold, hub_mode, emu_min, _aligned16(segs),
-                                   live=nz is not None, backward=True)
-            sc = sched_for(dev, role=_backward_role(dev, n, cnt, scale))
+                                   live=nz is not None, backward=True,
+                                   part0=PART0_SPARSE_BACKWARD
+                                   if role == "backward" and not any(gt.class_parts) else None)
+            sc = sched_for(dev, role=role)
             ev = _SideEvents(sc, K, side_timing is not None, side_trace is not None)
             sides = gt.sides_struct()
             try:
