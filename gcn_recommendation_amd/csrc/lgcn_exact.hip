@@ -68,6 +68,21 @@ constexpr int kHB = (1 << 24) - kSlack;
 constexpr int kC = 3 << 22;                   // a candidate's start mantissa (1.5 * 2^23)
 constexpr int kIdentEb = -32768;              // meta ebase of a block without a nonzero product
 static_assert(kNB == 16, "tables hold 16 binades (4 x int4 per (block, column))");
+
+// The walk's and the chain kernel's grids: (column or slice, row) — LGCN_ROWMAJOR=0 builds round
+// 5's (row, column) order for A/B
+#ifndef LGCN_ROWMAJOR
+#define LGCN_ROWMAJOR 1
+#endif
+#if LGCN_ROWMAJOR  // one dimension (a y extent is limited to 65535 rows): row * cols + column
+#define LGCN_GRID_COL(nc) (blockIdx.x % (uint32_t)(nc))
+#define LGCN_GRID_ROW(nc) (blockIdx.x / (uint32_t)(nc))
+#define LGCN_GRID_DIM(cols, rows) dim3((cols) * (rows))
+#else
+#define LGCN_GRID_COL(nc) blockIdx.y
+#define LGCN_GRID_ROW(nc) blockIdx.x
+#define LGCN_GRID_DIM(cols, rows) dim3((rows), (cols))
+#endif
 static_assert(LGCN_EMU_META_BYTES == 16, "meta record is one int4");
 
 // Records written by k_emu_blocks per (block, column) rc = block * d + column:
@@ -591,14 +606,18 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     // X elements (dynamic LDS, sized at launch)
     extern __shared__ __attribute__((aligned(16))) float s_dyn[];
     const int lane = threadIdx.x;
-    const int c = blockIdx.y;
+    // grid (column, row): a row's column waves are dispatched together, longest row first (the
+    // rows are in descending length), so a long row's last columns do not queue behind every
+    // shorter row's first ones
+    const int c = (int)LGCN_GRID_COL(d);
+    const uint32_t rix = LGCN_GRID_ROW(d);
 #ifdef LGCN_WALK_PRIO
     // issue priority over the co-resident waves of other kernels on this SIMD (build flag A/B)
     __builtin_amdgcn_s_setprio(LGCN_WALK_PRIO);
 #endif
     // a row the live-edge chains run (lgcn_live_rows flags it, aligned with `rows`) is theirs
-    if (live && live[blockIdx.x].n_blocks) return;
-    const lgcn_emu_row_t er = rows[blockIdx.x];
+    if (live && live[rix].n_blocks) return;
+    const lgcn_emu_row_t er = rows[rix];
     const int64_t fb = er.first_block;
     const int nb_all = er.n_blocks;
     // block k of the row holds edges [row_beg + k * B, min(.. + B, row_end)) (plan_emulation)
@@ -910,22 +929,22 @@ __global__ __launch_bounds__(64) void k_emu_walk(const lgcn_edge_t* __restrict__
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA lands after the wave is gone
 #ifdef LGCN_EMU_STATS
-    if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0)
+    if (lane == 0 && rix == 0 && c == 0)
         for (int k = 0; k < 16; ++k) g_emu_phase[k] += ph[k];
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_emu_stats[k], est[k]);
-    if (lane == 0 && blockIdx.x < 256) {
-        atomicAdd(&g_emu_row_stats[blockIdx.x][0], n_fast);
-        atomicAdd(&g_emu_row_stats[blockIdx.x][1], n_slow);
-        atomicAdd(&g_emu_row_stats[blockIdx.x][2], t_slow);
-        atomicMax(&g_emu_row_stats[blockIdx.x][3], __builtin_amdgcn_s_memtime() - t_start);
+    if (lane == 0 && rix < 256) {
+        atomicAdd(&g_emu_row_stats[rix][0], n_fast);
+        atomicAdd(&g_emu_row_stats[rix][1], n_slow);
+        atomicAdd(&g_emu_row_stats[rix][2], t_slow);
+        atomicMax(&g_emu_row_stats[rix][3], __builtin_amdgcn_s_memtime() - t_start);
     }
 #endif
     if (lane != 0) return;
     const int32_t row = er.row;
     float out = __uint_as_float(ab);
     if constexpr (MODE == LGCN_EPI_ROWS) {  // the chain value itself, to row i of the list
-        y[(int64_t)blockIdx.x * ldy + c] = out;
+        y[(int64_t)rix * ldy + c] = out;
         return;
     }
     if constexpr (MODE == LGCN_EPI_MEAN) {
@@ -967,7 +986,7 @@ int launch_walk(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
                 const float* stage, const lgcn_rows_t& x, float xdiv, const uint32_t* x_nz, float* y,
                 int64_t ldy, int32_t d, const lgcn_epilogue_t& ep, int slots,
                 const lgcn_emu_row_t* live, hipStream_t s) {
-    const dim3 grid((uint32_t)n_rows, (uint32_t)d);
+    const dim3 grid = LGCN_GRID_DIM((uint32_t)d, (uint32_t)n_rows);
     const size_t lds = (size_t)(2 * slots + 1) * 2 * LGCN_EMU_BLOCK * sizeof(float);
     if (lds > 56 * 1024) {
         // beyond the default dynamic-LDS limit: raise it once per kernel and DEVICE (the
@@ -1069,8 +1088,10 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     __shared__ __attribute__((aligned(16))) int32_t s_col[NR][64];
     __shared__ __attribute__((aligned(16))) float s_val[NR][64];
     const int lane = threadIdx.x;
-    const int c0 = blockIdx.y * W;
-    const lgcn_emu_row_t er = rows[blockIdx.x];
+    // grid (slice, row): a row's slices are dispatched together, longest row first
+    const int c0 = (int)LGCN_GRID_COL((d + W - 1) / W) * W;
+    const uint32_t rix = LGCN_GRID_ROW((d + W - 1) / W);
+    const lgcn_emu_row_t er = rows[rix];
     if (er.n_blocks <= 0) return;  // (a live-edge row left to the walk: lgcn_live_rows)
     const int32_t beg = blocks[er.first_block].beg;
     const int32_t end = blocks[er.first_block + er.n_blocks - 1].end;
@@ -1180,7 +1201,7 @@ __global__ __launch_bounds__(64) void k_chain_rows(const lgcn_edge_t* __restrict
     const int32_t row = er.row;
     float out = acc;
     if constexpr (MODE == LGCN_EPI_ROWS) {  // the chain value itself, to row i of the list
-        y[(int64_t)blockIdx.x * ldy + c] = out;
+        y[(int64_t)rix * ldy + c] = out;
         return;
     }
     if constexpr (MODE == LGCN_EPI_MEAN) {
@@ -1205,7 +1226,7 @@ int launch_chain(const lgcn_edge_t* edges, const lgcn_emu_block_t* blocks,
     // or more waves per row, each with twice the windows in flight of a 64-column wave
     // (16- and 8-column slices: the d/P columns of a featsplit shard — d=64 at P=4, P=8)
     const int w = d % 32 == 0 ? 32 : d % 16 == 0 ? 16 : 8;  // d % 8 == 0 (checked by the caller)
-    const dim3 grid((uint32_t)n_rows, (uint32_t)((d + w - 1) / w));
+    const dim3 grid = LGCN_GRID_DIM((uint32_t)((d + w - 1) / w), (uint32_t)n_rows);
     const bool seg1 = x.p0 == x.p1 && x.p1 == x.p2;
 #define LGCN_CH(W_, S_) \
     hipLaunchKernelGGL((k_chain_rows<MODE, XD, W_, S_>), grid, dim3(64), 0, s, edges, blocks, \
