@@ -191,6 +191,43 @@ def test_backward_hint_ring(gpu_device, monkeypatch, brand_graph):
         assert engine._hint_dense(gpu_device, n) is dense
 
 
+def test_sparse_backward_part0_cut(gpu_device, monkeypatch, brand_graph):
+    """The row-sparse backward's own part-0 cut (engine.PART0_SPARSE_BACKWARD, 2048 blocks at
+    C3; here 16 so that the brand graph's item hubs move from part 1 to part 0): once the hint
+    ring says G is row-sparse the backward's plans take it, the dense calls keep the forward's
+    cut, and every call is bitwise against the oracle."""
+    monkeypatch.setenv("LGCN_SIDES_MIN_NNZ", "0")
+    monkeypatch.setenv("LGCN_CHAIN_MAX", "2048")
+    monkeypatch.setenv("LGCN_CLASSES", "0")
+    monkeypatch.setattr(engine, "PART0_SPARSE_BACKWARD", 16)
+    seen = []
+    orig = engine._side_plans
+
+    def spy(*a, **kw):
+        seen.append(kw.get("part0"))
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(engine, "_side_plans", spy)
+    r, c, v, n = brand_graph
+    g = engine.graph_from_coo(_adj(r, c, v, n, gpu_device), sides=(U, U + I))
+    hp = g.side_hubs(128, mode="exact", emu_min=256)[3]
+    rows16, _ = hp.walk_parts(g.nnz, backward=True, part0=16)
+    rows_fwd, _ = hp.walk_parts(g.nnz, backward=True)
+    assert rows16[0] > rows_fwd[0] and rows16[1] == rows_fwd[1]  # the cut moves rows to part 0
+    rng = np.random.default_rng(17)
+    G = _e0(rng, "xavier", n, 64)
+    Gs = np.where(rng.random((n, 1)) < 0.01, G, 0.0).astype(np.float32)
+    for Gx in (Gs, G, Gs):
+        want = oracle.backward(r, c, v, Gx, 3)
+        segs = _segs(Gx, gpu_device)
+        seen.clear()
+        for _ in range(10):
+            got = engine.propagate_backward(g, segs, 3, **KW)
+            torch.cuda.synchronize()  # the hint of each call lands before the next
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+        assert seen[-1] == (16 if Gx is Gs else None), seen
+
+
 def test_lane1_shared_bitwise(gpu_device, monkeypatch, brand_graph):
     """LGCN_SCHED_LANE1_SHARED: lane 1 on the caller's stream and lane 0's aux streams reversed
     (two lanes of half-layers on three aux streams): forward and row-sparse / dense backward
