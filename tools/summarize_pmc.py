@@ -12,7 +12,7 @@ import re
 import sys
 from collections import defaultdict
 
-KEEP = ("k_layer", "k_emu_blocks", "k_emu_walk", "k_chain_rows")
+KEEP = ("k_layer", "k_emu_blocks", "k_emu_walk", "k_chain_rows", "k_score_topk")
 
 
 def short(name):
