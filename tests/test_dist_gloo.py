@@ -148,3 +148,21 @@ def test_balanced_bounds_and_layout():
     assert list(np.diff(cb)) == [8] * 8
     cb = D.feature_bounds(12, 8)
     assert cb[-1] == 12 and np.all(np.diff(cb) >= 1)
+
+
+def test_package_import_raises_hw_queues_under_torchrun():
+    """A `torchrun main.py` rank (WORLD_SIZE > 1) gets GPU_MAX_HW_QUEUES=16 from importing the
+    package (RCCL's streams would otherwise share the schedule's hardware queues, DESIGN §6);
+    a single process is left alone, and a larger setting is kept."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import os, gcn_recommendation_amd; print(os.environ.get('GPU_MAX_HW_QUEUES'))"
+    for env, want in (({"WORLD_SIZE": "2"}, "16"), ({"WORLD_SIZE": "1"}, "None"),
+                      ({"WORLD_SIZE": "4", "GPU_MAX_HW_QUEUES": "24"}, "24")):
+        e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "GPU_MAX_HW_QUEUES")}
+        e.update(env)
+        out = subprocess.run([sys.executable, "-c", code], cwd=root, env=e, capture_output=True,
+                             text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        assert out.stdout.strip() == want, (env, out.stdout)
