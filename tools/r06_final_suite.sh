@@ -7,5 +7,3 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -2 gpurun_out/final2/gpu_tests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" >> gpurun_out/final2/gpu_tests.log 2>&1 || exit 1
 tail -1 gpurun_out/final2/gpu_tests.log
-timeout -k 10 900 python -u bench.py > gpurun_out/final2/bench_c3.log 2>&1 || exit 1
-tail -1 gpurun_out/final2/bench_c3.log | cut -c1-400
